@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Benchmark of the fused flash-attention hot path on MI355X.
+
+Default (the driver's contract): BASELINE.json config 2 — full_1d fp16,
+B=8 H=16 d=64 Nq=Nk=4096, forward — metric "fwd TFLOP/s per GPU + MFMA util %".
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--no-cpu-baseline]
+
+For N>1 run under torch.distributed.run: one process per GPU, each rank runs
+its own shard of batch×head slices (no data-path collective; a gloo
+barrier / max-reduce over CPU tensors only brackets the timed region).
+c2/c3/c5: every rank processes the full config batch (weak scaling);
+c4: the config's b=1024 slices are split across ranks (strong scaling, as the
+config prescribes "batch-sharded across 8×MI355X").
+
+A step = one pass of the op over the rank's batch with inputs resident in HBM
+(c3: forward + backward).  Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from tf_flash_attention_amd import flash_attention as fa  # noqa: E402
+
+MFMA_PEAK = {"fp16": 2516.6, "fp32": 157.3, "fp64": 78.6}   # dense TFLOP/s (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    # name: (policy, seq_dims, dtype, batch, d, q_seq, k_seq, sync, ws, ls, causal, backward, scaling)
+    "c2": ("full", 1, torch.float16, (8, 16), 64, (4096,), (4096,), "none_front", 1, 0, False, False, "weak"),
+    "c3": ("causal", 1, torch.float16, (8, 16), 128, (8192,), (8192,), "none_front", 1, 0, False, True, "weak"),
+    "c4": ("local", 1, torch.float16, (64, 16), 64, (16384,), (16384,), "none_front", 256, 0, False, False, "strong"),
+    "c5": ("full", 2, torch.float32, (4, 8), 64, (64, 64), (128, 128), "scale_front", 1, 0, False, False, "weak"),
+}
+WORKLOAD = {
+    "c2": "full_1d fp16 B=8 H=16 d=64 Nq=Nk=4096 forward (BASELINE config 2)",
+    "c3": "causal_1d fp16 B=8 H=16 d=128 N=8192 forward+backward (BASELINE config 3)",
+    "c4": "local_1d fp16 window=256 B=64 H=16 d=64 N=16384 forward (BASELINE config 4)",
+    "c5": "full_2d fp32 B=4 H=8 d=64 (64,64)x(128,128) scale_front forward (BASELINE config 5)",
+}
+DTYPE_NAME = {torch.float16: "fp16", torch.float32: "fp32", torch.float64: "fp64"}
+
+
+def _dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def _call_forward(cfg, q, k, v):
+    policy, seq_dims, _, _, _, _, _, sync, ws, ls, causal, _, _ = cfg
+    return fa.attention_forward(policy, seq_dims, q, k, v, sync, ws, ls, causal)
+
+
+def _call_backward(cfg, q, k, v, o, l, m, do):
+    policy, seq_dims, _, _, _, _, _, sync, ws, ls, causal, _, _ = cfg
+    return fa.attention_backward(policy, seq_dims, q, k, v, o, l, m, do, sync, ws, ls, causal)
+
+
+def cpu_baseline(cfg, budget_s: float):
+    """The reference's naive (TF) CPU attention, restated in numpy fp32
+    (oracle.naive_attention_slice_f32, tests/test_1d.py:69-76), timed on a bounded
+    sample of (b,h) slices of the same workload; fp16 inputs upcast to fp32."""
+    from oracle import fa_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = 1
+    policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, _ = cfg
+    rng = np.random.default_rng(0)
+    nq, nk = int(np.prod(qs)), int(np.prod(ks))
+    prob = O.Problem(policy, seq_dims, sync, ws, ls, causal)
+    mask = None
+    if policy != "full":
+        mask = O.problem_mask(prob, list(qs), list(ks))
+    pairs = nq * nk if mask is None else int(mask.sum())
+    flops_slice = 2.0 * (d + d) * pairs
+    q = rng.uniform(-2, 2, (d, nq)).astype(np.float32)
+    k = rng.uniform(-2, 2, (d, nk)).astype(np.float32)
+    v = rng.uniform(-2, 2, (d, nk)).astype(np.float32)
+    O.naive_attention_slice_f32(q[:, :64], k[:, :64], v[:, :64])  # warm BLAS threads
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.naive_attention_slice_f32(q, k, v, mask)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= int(np.prod(batch)):
+            break
+    tflops = flops_slice * n / el / 1e12
+    return {"value": tflops, "unit": "TFLOP/s", "cores": int(cores), "kind": "port",
+            "sample": f"{n} of {int(np.prod(batch))} (b,h) slices of the workload, numpy fp32 naive attention "
+                      f"(einsum->softmax->einsum, tests/test_1d.py:69-76), {el:.1f}s; fp16 inputs upcast"}
+
+
+def load_traffic(workload_key: str):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/traffic_<key>.json),
+    written by tools/pmc_traffic.py; None if absent."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{workload_key}.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    args = ap.parse_args()
+
+    world, rank, local = _dist_env()
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    cfg = CONFIGS[args.config]
+    policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, scaling = cfg
+    b_total = int(np.prod(batch))
+    if scaling == "strong":
+        assert b_total % world == 0, "batch must divide across ranks"
+        b_rank = b_total // world
+    else:
+        b_rank = b_total
+    shape_q = (b_rank, d) + qs
+    shape_k = (b_rank, d) + ks
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    # U(-2,2) synthetic inputs generated on device (tests/test_base.py:170-173 distribution)
+    q = (torch.rand(shape_q, generator=g, device=dev, dtype=torch.float32) * 4 - 2).to(dt)
+    k = (torch.rand(shape_k, generator=g, device=dev, dtype=torch.float32) * 4 - 2).to(dt)
+    v = (torch.rand(shape_k, generator=g, device=dev, dtype=torch.float32) * 4 - 2).to(dt)
+    do = (torch.rand(shape_q, generator=g, device=dev, dtype=torch.float32) * 4 - 2).to(dt) if bwd else None
+
+    fwd_flops_rank = fa.estimate_forward_flops(policy, seq_dims, shape_q, shape_k, shape_k, sync, ws, ls, causal)
+    pairs_rank = fwd_flops_rank / (2.0 * (d + d))
+    bwd_flops_rank = 2.0 * (3 * d + 2 * d) * pairs_rank if bwd else 0.0
+    step_flops_rank = fwd_flops_rank + bwd_flops_rank
+
+    o = l = m = None
+
+    def step():
+        nonlocal o, l, m
+        o, l, m = _call_forward(cfg, q, k, v)
+        if bwd:
+            _call_backward(cfg, q, k, v, o, l, m, do)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    total_flops = step_flops_rank * world * args.steps
+    value = total_flops / elapsed / 1e12
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        dname = DTYPE_NAME[dt]
+        peak = MFMA_PEAK[dname]
+        achieved = step_flops_rank / (kern_ms * 1e-3) / 1e12  # one rank's launches / event-timed duration
+        traffic = load_traffic(args.config)
+        line = {
+            "metric": "fwd TFLOP/s per GPU + MFMA util %, fp16 full_1d d=64 seq=4096" if args.config == "c2"
+            else f"TFLOP/s ({args.config})",
+            "value": round(value, 3),
+            "unit": "TFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": scaling,
+            "vs_baseline": None,
+            "dtype": dname,
+            "data": "synthetic U(-2,2), generated on device",
+            "config": {"workload": WORKLOAD[args.config], "b_per_rank": b_rank, "d": d, "q_seq": list(qs),
+                       "k_seq": list(ks), "policy": policy, "sync_mode": sync,
+                       "parallelism": f"batch-shard x{world} (no collective)"},
+            "per_gpu_tflops": round(value / world, 3),
+            "mfma_util_pct": round(100.0 * achieved / peak, 2),
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "algorithmic_flops_per_launch": step_flops_rank,
+                         "event_ms_per_launch": round(kern_ms, 4)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_budget)
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

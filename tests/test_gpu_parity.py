@@ -1,0 +1,277 @@
+"""GPU parity: the HIP path (through the C ABI, via the reference-API mirror) vs
+the float64 oracle on identical dtype-rounded inputs.
+
+Tolerances (stated here, checked per element: |got - ref| <= ATOL*max|ref| + RTOL*|ref|):
+  fp16: forward O rtol 1e-3 / atol 1e-3*max|O|  (BASELINE.json north_star rtol=1e-3);
+        backward rtol 1e-3 / atol 2e-3*max|grad|
+  fp32: rtol 1e-5 / atol 1e-5*max  (north_star rtol=1e-5)
+  fp64: rtol 1e-10 / atol 1e-10*max
+l is checked with the same rtol (l for fp16 is fp32), m to one unit in the last
+place of T (it is the rounded row max).  The reference's own gate
+(rtol=atol=1e-3*N for fp16, 1e-6*N otherwise; tests/test_base.py:198-226) is far
+looser and is implied.  Rows that attend nothing must be exactly O=0, l=0,
+m=bytes 0xFA.
+"""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fa_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = {
+    np.float16: dict(fwd=(1e-3, 1e-3), bwd=(1e-3, 2e-3)),
+    np.float32: dict(fwd=(1e-5, 1e-5), bwd=(1e-5, 1e-5)),
+    np.float64: dict(fwd=(1e-10, 1e-10), bwd=(1e-10, 1e-10)),
+}
+TORCH = {np.float16: torch.float16, np.float32: torch.float32, np.float64: torch.float64}
+
+
+def _fa():
+    from tf_flash_attention_amd import flash_attention as fa
+    return fa
+
+
+def _close(name, got, ref, rtol, atol_rel):
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    scale = float(np.max(np.abs(ref))) if ref.size else 0.0
+    atol = atol_rel * max(scale, 1e-30)
+    err = np.abs(got - ref)
+    bad = err > atol + rtol * np.abs(ref)
+    assert np.isfinite(got).all(), f"{name}: non-finite output"
+    assert not bad.any(), (f"{name}: {bad.sum()} / {bad.size} elements off; max abs err {err.max():.3e}, "
+                           f"max|ref| {scale:.3e}, worst idx {np.unravel_index(np.argmax(err - rtol * np.abs(ref)), err.shape)}")
+    return float(err.max() / max(scale, 1e-30))
+
+
+def _call(policy, seq_dims, tq, tk, tv, mode, ws, ls, causal):
+    fa = _fa()
+    if policy == "full":
+        f = fa.full_1d if seq_dims == 1 else fa.full_2d
+        return f(tq, tk, tv, sync_mode=mode, returning_l_m=True)
+    if policy == "causal":
+        f = fa.causal_1d if seq_dims == 1 else fa.causal_2d
+        return f(tq, tk, tv, mode, returning_l_m=True)
+    f = fa.local_1d if seq_dims == 1 else fa.local_2d
+    return f(tq, tk, tv, ws, ls, causal, mode, returning_l_m=True)
+
+
+def run_case(dtype, policy, seq_dims, mode, batch, d, vd, qs, ks, ws=1, ls=0, causal=False, seed=0, bwd=True,
+             slices=None, inputs=None):
+    rng = np.random.default_rng(seed)
+    qs, ks = tuple(qs), tuple(ks)
+    if inputs is None:
+        Q = rng.uniform(-2, 2, tuple(batch) + (d,) + qs).astype(dtype)
+        K = rng.uniform(-2, 2, tuple(batch) + (d,) + ks).astype(dtype)
+        V = rng.uniform(-2, 2, tuple(batch) + (vd,) + ks).astype(dtype)
+        dO = rng.uniform(-2, 2, tuple(batch) + (vd,) + qs).astype(dtype)
+    else:
+        Q, K, V, dO = inputs
+    dev = torch.device("cuda:0")
+    tq = torch.from_numpy(Q).to(dev).requires_grad_(bwd)
+    tk = torch.from_numpy(K).to(dev).requires_grad_(bwd)
+    tv = torch.from_numpy(V).to(dev).requires_grad_(bwd)
+    o, l, m = _call(policy, seq_dims, tq, tk, tv, mode, ws, ls, causal)
+    if bwd:
+        o.backward(torch.from_numpy(dO).to(dev))
+    torch.cuda.synchronize()
+    prob = O.Problem(policy, seq_dims, mode, ws, ls, causal)
+    b = int(np.prod(batch))
+    flat = lambda x: x.reshape((b,) + x.shape[len(batch):])  # noqa: E731
+    sl = list(range(b)) if slices is None else list(slices)
+    Qf, Kf, Vf, dOf = flat(Q), flat(K), flat(V), flat(dO)
+    O64, L64, M64, has_any = O.forward_f64(Qf, Kf, Vf, prob, slices=sl)
+    rtol, atol = TOL[dtype]["fwd"]
+    og = flat(o.detach().cpu().numpy())[sl]
+    res = {"O": _close("O", og, O64, rtol, atol)}
+    # l, m
+    nq = int(np.prod(qs))
+    lg = flat(l.cpu().numpy()).reshape(b, nq)[sl].astype(np.float64)
+    mg = flat(m.cpu().numpy()).reshape(b, nq)[sl]
+    M64 = M64.reshape(len(sl), nq)
+    L64 = L64.reshape(len(sl), nq)
+    ha = has_any
+    if ha.any():
+        m_f = mg[:, ha].astype(np.float64)
+        ulp = np.abs(np.spacing(np.abs(M64[:, ha]).astype(dtype))).astype(np.float64)
+        assert (np.abs(m_f - M64[:, ha]) <= 2 * ulp + 1e-6 * np.abs(M64[:, ha]) + (1e-6 if dtype != np.float64 else 1e-12)).all(), "m"
+        l_ref = L64[:, ha] * np.exp(M64[:, ha] - m_f)    # relative to the stored m
+        _close("l", lg[:, ha], l_ref, max(rtol, 1e-6 if dtype == np.float16 else rtol), atol)
+    if (~ha).any():
+        assert (og.reshape(len(sl), vd, nq)[:, :, ~ha] == 0).all()
+        assert (lg[:, ~ha] == 0).all()
+        assert mg[:, ~ha].tobytes() == b"\xfa" * (mg[:, ~ha].size * np.dtype(dtype).itemsize)
+    if bwd:
+        dQ, dK, dV = O.backward_f64(Qf, Kf, Vf, dOf, prob, slices=sl)
+        rtol, atol = TOL[dtype]["bwd"]
+        res["dQ"] = _close("dQ", flat(tq.grad.cpu().numpy())[sl], dQ, rtol, atol)
+        res["dK"] = _close("dK", flat(tk.grad.cpu().numpy())[sl], dK, rtol, atol)
+        res["dV"] = _close("dV", flat(tv.grad.cpu().numpy())[sl], dV, rtol, atol)
+    return res
+
+
+DTYPES = [np.float16, np.float32, np.float64]
+
+
+# ---------------------------------------------------------------- config 1
+def test_config1_fixture():
+    import os
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1_full1d_f32.npz"))
+    fa = _fa()
+    dev = torch.device("cuda:0")
+    tq, tk, tv = (torch.from_numpy(f[n]).to(dev).requires_grad_(True) for n in ("Q", "K", "V"))
+    o, l, m = fa.full_1d(tq, tk, tv, returning_l_m=True)
+    o.backward(torch.from_numpy(f["dO"]).to(dev))
+    _close("O", o.detach().cpu().numpy(), f["O"], 1e-5, 1e-5)
+    _close("l", l.cpu().numpy(), f["l"], 1e-5, 1e-5)
+    _close("m", m.cpu().numpy(), f["m"], 1e-5, 1e-6)
+    for g, n in ((tq.grad, "dQ"), (tk.grad, "dK"), (tv.grad, "dV")):
+        _close(n, g.cpu().numpy(), f[n], 1e-5, 1e-5)
+
+
+# ------------------------------------------ the reference's test matrix
+# 15 registered cases + the unregistered CausalAttentionSyncModeNoneFront (tests/test_base.py:314-385)
+REF_CASES = [
+    ("full", "none_front", False, False),
+    ("causal", "none_front", False, False),
+    ("causal", "scale_front", False, False),
+    ("causal", "scale_end", False, False),
+] + [("local", mode, stride, causal) for stride, causal in ((False, False), (True, False), (False, True), (True, True))
+     for mode in ("none_front", "scale_front", "scale_end")]
+
+
+def _ref_window(seq_dims, qs, ks, stride):
+    # VanillaLocalPolicy: window = max(diff.shape) (tests/test_base.py:54-58)
+    window = max((1,) + tuple(qs) + tuple(ks) + (seq_dims,))
+    ls = int(np.log2(window)) if stride else 0
+    return window, ls
+
+
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
+@pytest.mark.parametrize("seq_dims", [1, 2])
+@pytest.mark.parametrize("case", REF_CASES, ids=lambda c: f"{c[0]}-{c[1]}-s{int(c[2])}-c{int(c[3])}")
+def test_reference_matrix(dtype, seq_dims, case):
+    policy, mode, stride, causal = case
+    rng = np.random.default_rng(hash((seq_dims,) + case) % 2**32)
+    d = int(rng.integers(8, 33))
+    if seq_dims == 1:
+        qs = (int(rng.integers(40, 400)),)
+        ks = (int(rng.integers(40, 400)),)
+        if dtype == np.float16:  # fp16 tests round the last seq dim to even (test_base.py:148-149)
+            qs, ks = (qs[0] // 2 * 2,), (ks[0] // 2 * 2,)
+    else:
+        qs = (int(rng.integers(4, 20)), int(rng.integers(4, 20)))
+        ks = (int(rng.integers(4, 20)), int(rng.integers(4, 20)))
+    ws, ls = _ref_window(seq_dims, qs, ks, stride)
+    run_case(dtype, policy, seq_dims, mode, (1, 3), d, d, qs, ks, ws, ls, causal, seed=1)
+
+
+# ------------------------------------------------- small windows / strides
+@pytest.mark.parametrize("dtype", [np.float16, np.float32], ids=lambda t: np.dtype(t).name)
+@pytest.mark.parametrize("seq_dims,qs,ks", [(1, (300,), (300,)), (1, (257,), (130,)), (2, (12, 13), (12, 13)),
+                                            (2, (16, 8), (8, 16))])
+@pytest.mark.parametrize("ws,ls,causal", [(1, 0, False), (2, 0, False), (8, 0, True), (37, 0, False), (2, 1, True),
+                                          (3, 3, False)])
+@pytest.mark.parametrize("mode", ["none_front", "scale_end"])
+def test_small_windows(dtype, seq_dims, qs, ks, ws, ls, causal, mode):
+    run_case(dtype, "local", seq_dims, mode, (2,), 16, 16, qs, ks, ws, ls, causal, seed=ws + ls)
+
+
+# ------------------------------------------------ fp16 MFMA-path shapes
+@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("policy", ["full", "causal", "local"])
+@pytest.mark.parametrize("nq,nk", [(256, 256), (320, 192), (130, 1000)])
+def test_f16_mfma_shapes(d, policy, nq, nk):
+    run_case(np.float16, policy, 1, "none_front", (2, 2), d, d, (nq,), (nk,), ws=33, ls=0, causal=False, seed=d)
+
+
+@pytest.mark.parametrize("d,vd", [(64, 32), (24, 64), (100, 100), (7, 3)])
+def test_odd_channels(d, vd):
+    for dt in DTYPES:
+        run_case(dt, "causal", 1, "scale_front", (1, 2), d, vd, (150,), (75,), seed=d)
+
+
+# --------------------------------------------------------------- edge cases
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
+@pytest.mark.parametrize("nq,nk", [(1, 1), (1, 77), (77, 1), (2, 3), (64, 64), (65, 63)])
+def test_tiny_sequences(dtype, nq, nk):
+    run_case(dtype, "full", 1, "none_front", (2,), 8, 8, (nq,), (nk,))
+    run_case(dtype, "causal", 1, "scale_end", (2,), 8, 8, (nq,), (nk,))
+
+
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
+def test_fully_masked_rows(dtype):
+    # causal scale_end with Nq > Nk leaves the first query rows with no key (orders of Q start below K's)
+    run_case(dtype, "causal", 1, "scale_end", (2,), 16, 16, (64,), (16,))
+    run_case(dtype, "local", 2, "scale_end", (1,), 16, 16, (4, 6), (6, 4), ws=1, ls=2, causal=True)
+
+
+def test_empty_batch_and_sequences():
+    fa = _fa()
+    dev = torch.device("cuda:0")
+    for shp_q, shp_k in (((0, 2, 8, 16), (0, 2, 8, 16)), ((1, 2, 8, 0), (1, 2, 8, 16))):
+        q = torch.zeros(shp_q, dtype=torch.float16, device=dev)
+        k = torch.zeros(shp_k, dtype=torch.float16, device=dev)
+        o, l, m = fa.full_1d(q, k, k, returning_l_m=True)
+        assert o.shape == shp_q and l.shape == shp_q[:2] + shp_q[3:]
+    # no keys at all: every row attends nothing
+    q = torch.ones((1, 1, 8, 5), dtype=torch.float32, device=dev)
+    k = torch.ones((1, 1, 8, 0), dtype=torch.float32, device=dev)
+    o, l, m = fa.full_1d(q, k, k, returning_l_m=True)
+    assert (o == 0).all() and (l == 0).all()
+    assert m.cpu().numpy().tobytes() == b"\xfa" * (5 * 4)
+
+
+def test_dtype_dispatch_and_l_dtype():
+    fa = _fa()
+    dev = torch.device("cuda:0")
+    for dt, ldt in ((torch.float16, torch.float32), (torch.float32, torch.float32), (torch.float64, torch.float64)):
+        x = torch.randn(1, 2, 8, 32, device=dev, dtype=dt)
+        o, l, m = fa.full_1d(x, x, x, returning_l_m=True)
+        assert o.dtype == dt and l.dtype == ldt and m.dtype == dt
+    with pytest.raises(TypeError):
+        x = torch.randn(1, 2, 8, 32, device=dev, dtype=torch.bfloat16)
+        fa.full_1d(x, x, x)
+
+
+def test_batch_dims_are_flattened_and_independent():
+    """Any batch rank (batch_shape may include heads) — slices are independent and
+    the result is bitwise identical whether computed together or shard by shard."""
+    fa = _fa()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    q = torch.rand((2, 3, 2, 64, 200), device=dev, generator=g).half() * 4 - 2
+    k = torch.rand((2, 3, 2, 64, 150), device=dev, generator=g).half() * 4 - 2
+    v = torch.rand((2, 3, 2, 64, 150), device=dev, generator=g).half() * 4 - 2
+    o = fa.causal_1d(q, k, v, "scale_front")
+    for i in range(2):
+        oi = fa.causal_1d(q[i], k[i], v[i], "scale_front")
+        assert torch.equal(o[i], oi)
+
+
+# --------------------------------------------- BASELINE configs (sampled)
+def test_config2_full_size_sampled():
+    """Config 2 at full size (b=128, N=4096, d=64, fp16): 3 slices checked against the oracle."""
+    run_case(np.float16, "full", 1, "none_front", (8, 16), 64, 64, (4096,), (4096,), bwd=False, slices=[0, 77, 127],
+             seed=1234)
+
+
+def test_config3_causal_d128_sampled():
+    """Config 3 shape at reduced batch (b=2): causal fp16 d=128 N=8192, forward + backward."""
+    run_case(np.float16, "causal", 1, "none_front", (1, 2), 128, 128, (8192,), (8192,), seed=3, slices=[1])
+
+
+def test_config4_local_window256_sampled():
+    """Config 4 shape at reduced batch: local ws=256 fp16 d=64 N=16384."""
+    run_case(np.float16, "local", 1, "none_front", (1, 2), 64, 64, (16384,), (16384,), ws=256, ls=0, causal=False,
+             seed=4, slices=[0])
+
+
+def test_config5_full2d_f32_sampled():
+    """Config 5 shape at reduced batch: full_2d fp32 (64,64) vs (128,128), scale_front."""
+    run_case(np.float32, "full", 2, "scale_front", (1, 2), 64, 64, (64, 64), (128, 128), seed=5, slices=[1])

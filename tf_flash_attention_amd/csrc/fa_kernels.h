@@ -1,0 +1,60 @@
+// fa_kernels.h — launch-argument structs and launcher entry points shared by
+// the C-ABI host layer (fa_api.hip) and the kernel translation units.
+#ifndef TF_FLASH_ATTENTION_AMD_FA_KERNELS_H_
+#define TF_FLASH_ATTENTION_AMD_FA_KERNELS_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fa_rules.h"
+
+namespace fa {
+
+struct FwdArgs {
+  const void* Q;
+  const void* K;
+  const void* V;
+  void* O;
+  void* l;
+  void* m;
+  int64_t b;
+  int32_t d, v_d;
+  double scale;  // 1/sqrt(d)
+  Rule rule;
+};
+
+struct BwdArgs {
+  const void* Q;
+  const void* K;
+  const void* V;
+  const void* O;
+  const void* l;
+  const void* m;
+  const void* dO;
+  void* dQ;
+  void* dK;
+  void* dV;
+  void* ws_dQ;   // accumulator: b*d*nq of AccT
+  void* ws_D;    // b*nq AccT
+  void* ws_lse;  // b*nq AccT
+  int64_t b;
+  int32_t d, v_d;
+  double scale;
+  Rule rule;
+};
+
+// generic (any dtype) path — fa_generic.hip
+hipError_t launch_fwd_generic(int dtype, const FwdArgs& a, hipStream_t s);
+hipError_t launch_bwd_generic(int dtype, const BwdArgs& a, hipStream_t s);
+int generic_max_channels(int dtype);
+
+// fp16 MFMA path — fa_fwd_f16.hip / fa_bwd_f16.hip.  Return hipErrorNotSupported
+// when the shape is outside what the MFMA kernels take (caller falls back).
+bool fwd_f16_supported(const FwdArgs& a);
+hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s);
+bool bwd_f16_supported(const BwdArgs& a);
+hipError_t launch_bwd_f16(const BwdArgs& a, hipStream_t s);
+
+}  // namespace fa
+
+#endif  // TF_FLASH_ATTENTION_AMD_FA_KERNELS_H_
