@@ -8,8 +8,9 @@ outputs that vanish analytically, e.g. dQ when a row attends a single key):
         backward rtol 1e-3 / atol 2e-3*max|grad|
   fp32: rtol 1e-5 / atol 1e-5*max  (north_star rtol=1e-5)
   fp64: rtol 1e-10 / atol 1e-10*max
-l is checked with the same rtol (l for fp16 is fp32), m to one unit in the last
-place of T (it is the rounded row max).  The reference's own gate
+l is checked with the same rtol (l for fp16 is fp32), m to two units in the last
+place of T (it is the rounded row max) — for fp16 plus rtol 1e-3 / atol 1e-3*max(|m|,1),
+since the fp16 kernel scores with Q pre-scaled by scale*log2(e) in fp16.  The reference's own gate
 (rtol=atol=1e-3*N for fp16, 1e-6*N otherwise; tests/test_base.py:198-226) is far
 looser and is implied.  Rows that attend nothing must be exactly O=0, l=0,
 m=bytes 0xFA.
@@ -102,7 +103,11 @@ def run_case(dtype, policy, seq_dims, mode, batch, d, vd, qs, ks, ws=1, ls=0, ca
     if ha.any():
         m_f = mg[:, ha].astype(np.float64)
         ulp = np.abs(np.spacing(np.abs(M64[:, ha]).astype(dtype))).astype(np.float64)
-        assert (np.abs(m_f - M64[:, ha]) <= 2 * ulp + 1e-6 * np.abs(M64[:, ha]) + (1e-6 if dtype != np.float64 else 1e-12)).all(), "m"
+        # m: 2 ulp of T, plus (fp16) the same rtol/atol-with-floor-1 as the other outputs — the
+        # fp16 kernel forms its scores from Q pre-scaled by scale*log2(e) in fp16 (~1e-4 abs)
+        m_tol = 2 * ulp + (1e-3 * np.maximum(np.abs(M64[:, ha]), 1.0) if dtype == np.float16
+                           else 1e-6 * np.abs(M64[:, ha]) + (1e-6 if dtype != np.float64 else 1e-12))
+        assert (np.abs(m_f - M64[:, ha]) <= m_tol).all(), f"m: max err {np.abs(m_f - M64[:, ha]).max():.3e}"
         l_ref = L64[:, ha] * np.exp(M64[:, ha] - m_f)    # relative to the stored m
         _close("l", lg[:, ha], l_ref, max(rtol, 1e-6 if dtype == np.float16 else rtol), atol)
     if (~ha).any():

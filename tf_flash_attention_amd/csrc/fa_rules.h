@@ -72,6 +72,20 @@ FA_HD bool check_orders(const Rule& r, int32_t qo, int32_t ko) {
   return true;
 }
 
+// Branch-free form of check_orders for per-element use inside kernels (every
+// condition evaluated, combined with bitwise &; compiles to v_cndmask, not
+// exec-mask branches).  Same result as check_orders for policy 1 and 2.
+FA_HD bool check_orders_bf(const Rule& r, int32_t qo, int32_t ko) {
+  if (r.policy == 1) return qo >= ko;  // wave-uniform branch
+  const int32_t rem = (1 << r.ls) - 1;
+  const int32_t d0 = iabs32((qo & (r.R0 - 1)) - (ko & (r.R0 - 1)));
+  const int32_t d1 = iabs32(((qo >> r.log2R0) & (r.R1 - 1)) - ((ko >> r.log2R0) & (r.R1 - 1)));
+  bool ok = ((d0 & rem) == 0) & ((d0 >> r.ls) < r.ws);
+  ok &= (r.seq_dims == 1) | (((d1 & rem) == 0) & ((d1 >> r.ls) < r.ws));
+  ok &= (r.look_ahead != 1) | (qo >= ko);
+  return ok;
+}
+
 FA_HD int32_t imin32(int32_t a, int32_t b) { return a < b ? a : b; }
 FA_HD int32_t imax32(int32_t a, int32_t b) { return a > b ? a : b; }
 

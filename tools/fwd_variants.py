@@ -1,0 +1,57 @@
+"""A/B timing of forward structure variants in ONE process (interleaved rounds),
+selected through FA_FWD_VARIANT.  Usage: python tools/fwd_variants.py [config] v1 v2 ..."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tf_flash_attention_amd import flash_attention as fa  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    args = sys.argv[1:]
+    cfgname = args.pop(0) if args and args[0].startswith("c") else "c2"
+    variants = args or ["-1"]
+    cfg = bench.CONFIGS[cfgname]
+    policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, _ = cfg
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(1234)
+    b = int(np.prod(batch))
+    q = (torch.rand((b, d) + qs, generator=g, device=dev) * 4 - 2).to(dt)
+    k = (torch.rand((b, d) + ks, generator=g, device=dev) * 4 - 2).to(dt)
+    v = (torch.rand((b, d) + ks, generator=g, device=dev) * 4 - 2).to(dt)
+    flops = fa.estimate_forward_flops(policy, seq_dims, q.shape, k.shape, v.shape, sync, ws, ls, causal)
+    ref = None
+    res = {vv: [] for vv in variants}
+    for rnd in range(3):
+        for vv in variants:
+            os.environ["FA_FWD_VARIANT"] = vv
+            for _ in range(3):
+                o, l, m = fa.attention_forward(policy, seq_dims, q, k, v, sync, ws, ls, causal)
+            torch.cuda.synchronize()
+            if rnd == 0:
+                if ref is None:
+                    ref = o.float()
+                err = (o.float() - ref).abs().max().item()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+            for a_, b_ in evs:
+                a_.record()
+                fa.attention_forward(policy, seq_dims, q, k, v, sync, ws, ls, causal)
+                b_.record()
+            torch.cuda.synchronize()
+            ms = float(np.median([a_.elapsed_time(b_) for a_, b_ in evs]))
+            res[vv].append(ms)
+            if rnd == 0:
+                print(f"variant {vv}: max|o - o_first| = {err:.3e}", flush=True)
+    for vv in variants:
+        ms = min(res[vv])
+        print(json.dumps({"config": cfgname, "variant": vv, "ms": [round(x, 4) for x in res[vv]],
+                          "tflops": round(flops / ms / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
