@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from tf_flash_attention_amd import flash_attention as fa  # noqa: E402
+from tf_flash_attention_amd import shard  # noqa: E402
 
 MFMA_PEAK = {"fp16": 2516.6, "fp32": 157.3, "fp64": 78.6}   # dense TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
@@ -50,13 +51,6 @@ WORKLOAD = {
     "c5": "full_2d fp32 B=4 H=8 d=64 (64,64)x(128,128) scale_front forward (BASELINE config 5)",
 }
 DTYPE_NAME = {torch.float16: "fp16", torch.float32: "fp32", torch.float64: "fp64"}
-
-
-def _dist_env():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    return world, rank, local
 
 
 def _call_forward(cfg, q, k, v):
@@ -126,23 +120,25 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     args = ap.parse_args()
 
-    world, rank, local = _dist_env()
+    world, rank, local = shard.dist_env()
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; modulo only matters when rehearsing N ranks on fewer GPUs
+    ndev = max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
 
     cfg = CONFIGS[args.config]
     policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, scaling = cfg
     b_total = int(np.prod(batch))
-    if scaling == "strong":
-        assert b_total % world == 0, "batch must divide across ranks"
-        b_rank = b_total // world
-    else:
+    if scaling == "strong":  # the config's slices split across ranks (contiguous slabs, no collective)
+        s0, s1 = shard.shard_range(b_total, world, rank)
+        b_rank = s1 - s0
+    else:                    # every rank runs the full config batch
         b_rank = b_total
     shape_q = (b_rank, d) + qs
     shape_k = (b_rank, d) + ks
@@ -188,10 +184,10 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
     if dist:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-    total_flops = step_flops_rank * world * args.steps
+        elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms])
+        total_flops = shard.sum_over_ranks([step_flops_rank])[0] * args.steps
+    else:
+        total_flops = step_flops_rank * args.steps
     value = total_flops / elapsed / 1e12
     ms_per_step = elapsed / args.steps * 1e3
 
