@@ -190,12 +190,19 @@ def test_small_windows(dtype, seq_dims, qs, ks, ws, ls, causal, mode):
     run_case(dtype, "local", seq_dims, mode, (2,), 16, 16, qs, ks, ws, ls, causal, seed=ws + ls)
 
 
-# ------------------------------------------------ fp16 MFMA-path shapes
+# ------------------------------------------- fp16 / fp32 MFMA-path shapes
 @pytest.mark.parametrize("d", [32, 64, 128])
 @pytest.mark.parametrize("policy", ["full", "causal", "local"])
 @pytest.mark.parametrize("nq,nk", [(256, 256), (320, 192), (130, 1000)])
 def test_f16_mfma_shapes(d, policy, nq, nk):
     run_case(np.float16, policy, 1, "none_front", (2, 2), d, d, (nq,), (nk,), ws=33, ls=0, causal=False, seed=d)
+
+
+@pytest.mark.parametrize("d", [16, 32, 48, 64, 96, 128])
+@pytest.mark.parametrize("policy", ["full", "causal", "local"])
+@pytest.mark.parametrize("nq,nk", [(256, 256), (130, 1001)])
+def test_f32_mfma_shapes(d, policy, nq, nk):
+    run_case(np.float32, policy, 1, "scale_end", (2, 1), d, d, (nq,), (nk,), ws=41, ls=0, causal=True, seed=d + 1)
 
 
 @pytest.mark.parametrize("d,vd", [(64, 32), (24, 64), (100, 100), (7, 3)])

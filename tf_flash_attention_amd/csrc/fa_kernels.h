@@ -53,6 +53,9 @@ int generic_max_channels(int dtype);
 bool fwd_f16_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s);
 bool bwd_f16_supported(const BwdArgs& a);
+// fp32 MFMA forward — fa_fwd_f32.hip
+bool fwd_f32_supported(const FwdArgs& a);
+hipError_t launch_fwd_f32(const FwdArgs& a, hipStream_t s);
 hipError_t launch_bwd_f16(const BwdArgs& a, hipStream_t s);
 
 }  // namespace fa
