@@ -99,6 +99,21 @@ def cpu_baseline(cfg, budget_s: float):
                       f"(einsum->softmax->einsum, tests/test_1d.py:69-76), {el:.1f}s; fp16 inputs upcast"}
 
 
+def algorithmic_bytes(cfg, b):
+    """(read, write) HBM bytes one step must move (SURVEY.md §8(d)).  Forward: Q,K,V in;
+    O, l, m out.  Backward adds Q,K,V,O,dO,l,m in; dQ,dK,dV out."""
+    policy, seq_dims, dt, batch, d, qs, ks, *_ = cfg
+    bwd = cfg[11]
+    nq, nk = int(np.prod(qs)), int(np.prod(ks))
+    t = torch.tensor([], dtype=dt).element_size()
+    lt = 4 if t == 2 else t
+    rd, wr = b * (nq * d + 2 * nk * d) * t, b * (nq * d * t + nq * (lt + t))
+    if bwd:
+        rd += b * ((3 * nq * d + 2 * nk * d) * t + nq * (lt + t))
+        wr += b * (nq * d + 2 * nk * d) * t
+    return rd, wr
+
+
 def load_traffic(workload_key: str):
     """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/traffic_<key>.json),
     written by tools/pmc_traffic.py; None if absent."""
@@ -196,6 +211,18 @@ def main():
         peak = MFMA_PEAK[dname]
         achieved = step_flops_rank / (kern_ms * 1e-3) / 1e12  # one rank's launches / event-timed duration
         traffic = load_traffic(args.config)
+        rd, wr = algorithmic_bytes(cfg, b_rank)
+        alg_bytes = rd + wr
+        # the binding roof: time at MFMA peak vs time at HBM peak for the algorithmic work
+        hbm_bound = alg_bytes / (HBM_PEAK_GBS * 1e9) > step_flops_rank / (peak * 1e12)
+        if hbm_bound:
+            roof = {"bound": "hbm", "achieved": round(alg_bytes / (kern_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s"}
+        else:
+            roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s"}
+        roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+        roof.update({"traffic": traffic, "algorithmic_flops_per_launch": step_flops_rank,
+                     "algorithmic_bytes_per_launch": alg_bytes, "event_ms_per_launch": round(kern_ms, 4)})
         line = {
             "metric": "fwd TFLOP/s per GPU + MFMA util %, fp16 full_1d d=64 seq=4096" if args.config == "c2"
             else f"TFLOP/s ({args.config})",
@@ -215,10 +242,7 @@ def main():
                        "parallelism": f"batch-shard x{world} (no collective)"},
             "per_gpu_tflops": round(value / world, 3),
             "mfma_util_pct": round(100.0 * achieved / peak, 2),
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "algorithmic_flops_per_launch": step_flops_rank,
-                         "event_ms_per_launch": round(kern_ms, 4)},
+            "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_budget)

@@ -181,8 +181,8 @@ def test_reference_matrix(dtype, seq_dims, case):
 
 # ------------------------------------------------- small windows / strides
 @pytest.mark.parametrize("dtype", [np.float16, np.float32], ids=lambda t: np.dtype(t).name)
-@pytest.mark.parametrize("seq_dims,qs,ks", [(1, (300,), (300,)), (1, (257,), (130,)), (2, (12, 13), (12, 13)),
-                                            (2, (16, 8), (8, 16))])
+@pytest.mark.parametrize("seq_dims,qs,ks", [(1, (300,), (300,)), (1, (257,), (130,)), (1, (130,), (517,)),
+                                            (2, (12, 13), (12, 13)), (2, (16, 8), (8, 16))])
 @pytest.mark.parametrize("ws,ls,causal", [(1, 0, False), (2, 0, False), (8, 0, True), (37, 0, False), (2, 1, True),
                                           (3, 3, False)])
 @pytest.mark.parametrize("mode", ["none_front", "scale_end"])
@@ -203,6 +203,15 @@ def test_f16_mfma_shapes(d, policy, nq, nk):
 @pytest.mark.parametrize("nq,nk", [(256, 256), (130, 1001)])
 def test_f32_mfma_shapes(d, policy, nq, nk):
     run_case(np.float32, policy, 1, "scale_end", (2, 1), d, d, (nq,), (nk,), ws=41, ls=0, causal=True, seed=d + 1)
+
+
+# 1d local bands at MFMA sizes: the interval-rule path (per-lane key interval, empty tiles skipped)
+@pytest.mark.parametrize("dtype", [np.float16, np.float32], ids=lambda t: np.dtype(t).name)
+@pytest.mark.parametrize("ws,causal", [(64, False), (100, True), (256, False), (300, True)])
+@pytest.mark.parametrize("mode,nq,nk", [("none_front", 1500, 1500), ("scale_front", 700, 1500),
+                                        ("scale_end", 1500, 600)])
+def test_local_band_mfma(dtype, ws, causal, mode, nq, nk):
+    run_case(dtype, "local", 1, mode, (2,), 64, 64, (nq,), (nk,), ws, 0, causal, seed=ws)
 
 
 @pytest.mark.parametrize("d,vd", [(64, 32), (24, 64), (100, 100), (7, 3)])

@@ -98,7 +98,11 @@ __device__ __forceinline__ u32x4 load_chunk(const __half* row, int e, int n, boo
 
 // One workgroup = NW waves = 32*NW query rows of one (batch, head) slice.
 //   POL  0: full policy (no rule mask; only the nk tail is masked)
-//        1: causal / local (tile classification + per-element rule on mixed tiles)
+//        1: interval rules (causal, 1d unit-stride local): each query's allowed keys
+//           are an index interval [klo, khi]; the tile class is two scalar compares
+//           against the wave's bounds and the mixed-tile mask one unsigned compare
+//        2: other local rules (2d, strided): tile_class + per-element rule check
+//   Tiles with no allowed pair for a wave are skipped by that wave (no MFMAs).
 //   FAST d == v_d == D and K/V rows 16-byte aligned (nk % 8 == 0): unguarded
 //        dwordx4 staging.
 // Scores are produced directly as exp2 arguments: Q is pre-scaled by
@@ -136,6 +140,52 @@ __global__ __launch_bounds__(NW * 64, waves_per_eu(D, F)) void fwd_f16_kernel(Fw
   const bool qvec = ((nq & 7) == 0) && ((reinterpret_cast<uintptr_t>(a.Q) & 15) == 0);
   const float c2 = (float)a.scale * kLog2e;
 
+  // ---- key range of this query block (rule-bounded)
+  const int qlast = min(q0 + kBM, nq) - 1;
+  int kb = 0, ke = nk;
+  if (POL != 0) k_range_for_q_block(a.rule, q0, qlast, &kb, &ke);
+  const int kt0 = (kb / kBN) * kBN;
+  const int ntiles = (ke > kb) ? (ke - kt0 + kBN - 1) / kBN : 0;
+
+  // ---- register staging of one K/V tile (16-B chunks; chunk = 8 keys of one channel row)
+  auto load_into = [&](u32x4 (&kr)[kCPT], u32x4 (&vr)[kCPT], int k0) {
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const int idx = tid + kThr * j, c = idx >> 3, m = idx & 7;
+      const bool in = (kChunks % kThr == 0) || idx < kChunks;
+      const int e = k0 + 8 * m;
+      if (FAST && (kChunks % kThr == 0) && k0 + kBN <= nk) {  // whole tile in range: unguarded
+        kr[j] = load16(K + (int64_t)c * nk + e);
+        vr[j] = load16(V + (int64_t)c * nk + e);
+      } else if (FAST) {
+        kr[j] = (in && e < nk) ? load16(K + (int64_t)c * nk + e) : u32x4{0, 0, 0, 0};
+        vr[j] = (in && e < nk) ? load16(V + (int64_t)c * nk + e) : u32x4{0, 0, 0, 0};
+      } else {
+        kr[j] = (in && c < d) ? load_chunk(K + (int64_t)c * nk, e, nk, false) : u32x4{0, 0, 0, 0};
+        vr[j] = (in && c < vd) ? load_chunk(V + (int64_t)c * nk, e, nk, false) : u32x4{0, 0, 0, 0};
+      }
+    }
+  };
+  auto store_from = [&](const u32x4 (&kr)[kCPT], const u32x4 (&vr)[kCPT], int buf) {
+    lds_char_t* kbuf = smem + buf * S::kBuf;
+    lds_char_t* vbuf = kbuf + S::kK;
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const int idx = tid + kThr * j, c = idx >> 3, m = idx & 7;
+      if ((kChunks % kThr == 0) || idx < kChunks) {
+        // K: [c][64 keys], 64-B halves swapped on rows with c&2 (conflict-free tr reads)
+        *reinterpret_cast<lds_u32x4_t*>(kbuf + c * 128 + ((m * 16) ^ ((c & 2) << 5))) = kr[j];
+        // V: [key/4][v][4] slabs -> the PV operand is a plain conflict-free ds_read_b64
+        *reinterpret_cast<lds_u32x2_t*>(vbuf + ((2 * m) * (D + kVPad) + c) * 8) = vr[j].xy;
+        *reinterpret_cast<lds_u32x2_t*>(vbuf + ((2 * m + 1) * (D + kVPad) + c) * 8) = vr[j].zw;
+      }
+    }
+  };
+  // prologue loads of tiles 0 and 1 are in flight together with the Q tile
+  u32x4 kreg[kCPT], vreg[kCPT], kreg1[kCPT], vreg1[kCPT];
+  if (ntiles > 0) load_into(kreg, vreg, kt0);
+  if (ntiles > 1) load_into(kreg1, vreg1, kt0 + kBN);
+
   // ---- Q tile [D][BM] -> LDS (64-B blocks XOR-swizzled by c&3: conflict-free tr reads)
   for (int idx = tid; idx < D * (kBM / 8); idx += kThr) {
     const int c = idx / (kBM / 8), m = idx % (kBM / 8);
@@ -160,53 +210,39 @@ __global__ __launch_bounds__(NW * 64, waves_per_eu(D, F)) void fwd_f16_kernel(Fw
   }
   __syncthreads();  // the Q region is reused by the K/V ring
 
-  // ---- key range of this query block (rule-bounded) and per-lane query order
-  const int qlast = min(q0 + kBM, nq) - 1;
-  int kb = 0, ke = nk;
-  if (POL != 0) k_range_for_q_block(a.rule, q0, qlast, &kb, &ke);
-  const int kt0 = (kb / kBN) * kBN;
-  const int ntiles = (ke > kb) ? (ke - kt0 + kBN - 1) / kBN : 0;
   const int wq0 = q0 + 32 * w;
   const int wq1 = min(wq0 + 31, nq - 1);
   const bool wave_active = wq0 < nq;
   const int qi = wq0 + r;
-  const int qo = (POL != 0 && qi < nq) ? seq_order(a.rule.q, a.rule, qi) : 0;
+  const int qo = (POL == 2 && qi < nq) ? seq_order(a.rule.q, a.rule, qi) : 0;
+  // POL 1 (interval rules): this lane's allowed keys [klo, klo + kspan) and the wave's
+  // bounds on them (both ends are non-decreasing in the query, so lanes 0 / last bound them)
+  int klo = 0, kspan = 0, wlo_min = 0, wlo_max = 0, whi_min = 0, whi_max = 0;
+  if (POL == 1 && wave_active) {
+    int khi;
+    key_interval(a.rule, min(qi, nq - 1), &klo, &khi);
+    kspan = max(khi - klo + 1, 0);
+    const int last = min(31, nq - 1 - wq0);
+    wlo_min = __builtin_amdgcn_readfirstlane(klo);
+    whi_min = __builtin_amdgcn_readfirstlane(khi);
+    wlo_max = __builtin_amdgcn_readlane(klo, last);
+    whi_max = __builtin_amdgcn_readlane(khi, last);
+  }
+  // tile class for this wave: 0 no allowed pair (skipped), 1 mixed (per-element mask), 2 all
+  auto tcls = [&](int k0) -> int {
+    const int k1 = k0 + kBN - 1;
+    if (!wave_active) return 0;
+    if (POL == 0) return k1 < nk ? 2 : 1;
+    if (POL == 1) {
+      if (wlo_min > k1 || whi_max < k0) return 0;
+      return (wlo_max <= k0 && whi_min >= k1) ? 2 : 1;
+    }
+    const int c = tile_class(a.rule, wq0, wq1, k0, min(k1, nk - 1));
+    return (c == 2 && k1 >= nk) ? 1 : c;
+  };
 
-  // ---- register staging of one K/V tile (16-B chunks; chunk = 8 keys of one channel row)
-  u32x4 kreg[kCPT], vreg[kCPT];
-  auto load_tile = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < kCPT; ++j) {
-      const int idx = tid + kThr * j, c = idx >> 3, m = idx & 7;
-      const bool in = (kChunks % kThr == 0) || idx < kChunks;
-      const int e = k0 + 8 * m;
-      if (FAST && (kChunks % kThr == 0) && k0 + kBN <= nk) {  // whole tile in range: unguarded
-        kreg[j] = load16(K + (int64_t)c * nk + e);
-        vreg[j] = load16(V + (int64_t)c * nk + e);
-      } else if (FAST) {
-        kreg[j] = (in && e < nk) ? load16(K + (int64_t)c * nk + e) : u32x4{0, 0, 0, 0};
-        vreg[j] = (in && e < nk) ? load16(V + (int64_t)c * nk + e) : u32x4{0, 0, 0, 0};
-      } else {
-        kreg[j] = (in && c < d) ? load_chunk(K + (int64_t)c * nk, e, nk, false) : u32x4{0, 0, 0, 0};
-        vreg[j] = (in && c < vd) ? load_chunk(V + (int64_t)c * nk, e, nk, false) : u32x4{0, 0, 0, 0};
-      }
-    }
-  };
-  auto store_tile = [&](int buf) {
-    lds_char_t* kbuf = smem + buf * S::kBuf;
-    lds_char_t* vbuf = kbuf + S::kK;
-#pragma unroll
-    for (int j = 0; j < kCPT; ++j) {
-      const int idx = tid + kThr * j, c = idx >> 3, m = idx & 7;
-      if ((kChunks % kThr == 0) || idx < kChunks) {
-        // K: [c][64 keys], 64-B halves swapped on rows with c&2 (conflict-free tr reads)
-        *reinterpret_cast<lds_u32x4_t*>(kbuf + c * 128 + ((m * 16) ^ ((c & 2) << 5))) = kreg[j];
-        // V: [key/4][v][4] slabs -> the PV operand is a plain conflict-free ds_read_b64
-        *reinterpret_cast<lds_u32x2_t*>(vbuf + ((2 * m) * (D + kVPad) + c) * 8) = vreg[j].xy;
-        *reinterpret_cast<lds_u32x2_t*>(vbuf + ((2 * m + 1) * (D + kVPad) + c) * 8) = vreg[j].zw;
-      }
-    }
-  };
+  auto load_tile = [&](int k0) { load_into(kreg, vreg, k0); };
+  auto store_tile = [&](int buf) { store_from(kreg, vreg, buf); };
 
   floatx16 acc_o[D / 32];
 #pragma unroll
@@ -242,18 +278,23 @@ __global__ __launch_bounds__(NW * 64, waves_per_eu(D, F)) void fwd_f16_kernel(Fw
 
   // Rule/tail mask, row max and (lazy) rebase of the scores of tile `it` (after
   // this, exp2(st) are the tile's probabilities relative to m_run).
-  auto prepare = [&](int it, floatx16 (&st)[2], floatx16 (&nxt)[2], bool has_next) {
+  auto prepare = [&](int it, int cls, floatx16 (&st)[2], floatx16 (&nxt)[2], bool has_next) {
     const int k0 = kt0 + it * kBN;
-    int cls = 2;
-    if (POL != 0) cls = wave_active ? tile_class(a.rule, wq0, wq1, k0, min(k0 + kBN, nk) - 1) : 0;
-    if ((POL != 0 && cls != 2) || k0 + kBN > nk) {  // mixed / empty / tail tile: per-element mask
+    if (cls == 1) {  // mixed / tail tile: per-element mask
+      const int base = k0 + 4 * h - klo;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int key = k0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
-          bool ok = key < nk;
-          if (POL != 0) ok &= (cls != 0) & (check_orders_bf(a.rule, qo, seq_order(a.rule.k, a.rule, key)) | (cls == 2));
+          const int off = 32 * t + (i & 3) + 8 * (i >> 2);
+          bool ok;
+          if (POL == 1) {
+            ok = (unsigned)(base + off) < (unsigned)kspan;
+          } else {
+            const int key = k0 + off + 4 * h;
+            ok = key < nk;
+            if (POL == 2) ok &= check_orders_bf(a.rule, qo, seq_order(a.rule.k, a.rule, key));
+          }
           st[t][i] = ok ? st[t][i] : kNegInf;
         }
     }
@@ -337,15 +378,11 @@ __global__ __launch_bounds__(NW * 64, waves_per_eu(D, F)) void fwd_f16_kernel(Fw
   // ---- prologue: tiles 0, 1 in the ring, tile 2 in registers, tile 0 scored
   floatx16 stA[2], stB[2];
   if (ntiles > 0) {
-    load_tile(kt0);
     store_tile(0);
-    if (ntiles > 1) {
-      load_tile(kt0 + kBN);
-      store_tile(1);
-    }
+    if (ntiles > 1) store_from(kreg1, vreg1, 1);
     if (ntiles > 2) load_tile(kt0 + 2 * kBN);
     __syncthreads();
-    qk(0, stA);
+    if (tcls(kt0) != 0) qk(0, stA);
   }
   // iteration it: ring slot it%3 holds tile it (V read now), slot (it+1)%3 tile it+1
   // (K read now), slot (it+2)%3 receives tile it+2.  One branch-free region per
@@ -360,10 +397,13 @@ __global__ __launch_bounds__(NW * 64, waves_per_eu(D, F)) void fwd_f16_kernel(Fw
       store_tile(s2);
       if (it + 3 < ntiles) load_tile(kt0 + (it + 3) * kBN);
     }
-    const bool has_next = it + 1 < ntiles;
-    if (has_next) qk(s1, nxt);   // Sᵀ MFMAs of tile it+1 enter the matrix pipe first
-    prepare(it, cur, nxt, has_next);
-    exp_pv(cur, slot);
+    const int ccur = tcls(kt0 + it * kBN);
+    const int cnxt = it + 1 < ntiles ? tcls(kt0 + (it + 1) * kBN) : 0;
+    if (cnxt != 0) qk(s1, nxt);   // Sᵀ MFMAs of tile it+1 enter the matrix pipe first
+    if (ccur != 0) {              // tiles without an allowed pair for this wave are skipped
+      prepare(it, ccur, cur, nxt, cnxt != 0);
+      exp_pv(cur, slot);
+    }
     if (F & kFSched) {  // MFMA / VALU interleave for the region (cdna_hip_programming.md T19)
 #pragma unroll
       for (int i = 0; i < 2 * (D / 16) + 4 * (D / 32); ++i) {
@@ -413,9 +453,10 @@ hipError_t launch_t(const FwdArgs& a, hipStream_t s) {
   const int smem = S::kTotal;
   const bool fast = a.d == D && a.v_d == D && (a.rule.k.n % 8 == 0) &&
                     (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) && (reinterpret_cast<uintptr_t>(a.V) % 16 == 0);
-  const bool full = a.rule.policy == 0;
-  auto kern = full ? (fast ? fwd_f16_kernel<D, NW, 0, true, F> : fwd_f16_kernel<D, NW, 0, false, F>)
-                   : (fast ? fwd_f16_kernel<D, NW, 1, true, F> : fwd_f16_kernel<D, NW, 1, false, F>);
+  const int pol = a.rule.policy == 0 ? 0 : (rule_is_interval(a.rule) ? 1 : 2);
+  auto kern = pol == 0 ? (fast ? fwd_f16_kernel<D, NW, 0, true, F> : fwd_f16_kernel<D, NW, 0, false, F>)
+            : pol == 1 ? (fast ? fwd_f16_kernel<D, NW, 1, true, F> : fwd_f16_kernel<D, NW, 1, false, F>)
+                       : (fast ? fwd_f16_kernel<D, NW, 2, true, F> : fwd_f16_kernel<D, NW, 2, false, F>);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      smem);
   if (e != hipSuccess) return e;
@@ -449,7 +490,11 @@ hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s) {
       case 800: return launch_t<64, 8, 0>(a, s);
       case 808: return launch_t<64, 8, 8>(a, s);
       case 840: return launch_t<64, 8, 40>(a, s);
-      default: return launch_t<64, 8, 8>(a, s);
+      default:
+        // local bands: ~10 key tiles per block, so block prologue/epilogue matter;
+        // 4-wave blocks let two blocks per CU cover each other's (c4: 5.2 vs 5.9 ms)
+        if (a.rule.policy == 2) return launch_t<64, 4, 8>(a, s);
+        return launch_t<64, 8, 8>(a, s);
     }
   }
   return launch_t<128, 4, 8>(a, s);

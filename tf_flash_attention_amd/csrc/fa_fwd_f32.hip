@@ -84,7 +84,19 @@ __global__ __launch_bounds__(kThreads, D >= 128 ? 1 : 2) void fwd_f32_kernel(Fwd
   const int wq1 = min(wq0 + 31, nq - 1);
   const bool wave_active = wq0 < nq;
   const int qi = wq0 + r;
-  const int qo = (POL != 0 && qi < nq) ? seq_order(a.rule.q, a.rule, qi) : 0;
+  const int qo = (POL == 2 && qi < nq) ? seq_order(a.rule.q, a.rule, qi) : 0;
+  // POL 1 (interval rules, see fa_fwd_f16.hip): lane key interval + wave bounds
+  int klo = 0, kspan = 0, wlo_min = 0, wlo_max = 0, whi_min = 0, whi_max = 0;
+  if (POL == 1 && wave_active) {
+    int khi;
+    key_interval(a.rule, min(qi, nq - 1), &klo, &khi);
+    kspan = max(khi - klo + 1, 0);
+    const int last = min(31, nq - 1 - wq0);
+    wlo_min = __builtin_amdgcn_readfirstlane(klo);
+    whi_min = __builtin_amdgcn_readfirstlane(khi);
+    wlo_max = __builtin_amdgcn_readlane(klo, last);
+    whi_max = __builtin_amdgcn_readlane(khi, last);
+  }
   const bool kvec = ((nk & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.K) & 15) == 0) &&
                     ((reinterpret_cast<uintptr_t>(a.V) & 15) == 0);
 
@@ -145,9 +157,15 @@ __global__ __launch_bounds__(kThreads, D >= 128 ? 1 : 2) void fwd_f32_kernel(Fwd
     if (it + 1 < ntiles) load_tile(k0 + kBN);
     __syncthreads();
 
-    int cls = 2;
-    if (POL != 0) cls = wave_active ? tile_class(a.rule, wq0, wq1, k0, min(k0 + kBN, nk) - 1) : 0;
-    else if (!wave_active) cls = 0;
+    const int k1 = k0 + kBN - 1;
+    int cls;
+    if (!wave_active) cls = 0;
+    else if (POL == 0) cls = k1 < nk ? 2 : 1;
+    else if (POL == 1) cls = (wlo_min > k1 || whi_max < k0) ? 0 : ((wlo_max <= k0 && whi_min >= k1) ? 2 : 1);
+    else {
+      cls = tile_class(a.rule, wq0, wq1, k0, min(k1, nk - 1));
+      if (cls == 2 && k1 >= nk) cls = 1;
+    }
     if (cls == 0) continue;
     const lds_f_t* kbuf = smem + (it & 1) * S::kBuf;
     const lds_f_t* vbuf = kbuf + S::kK;
@@ -161,14 +179,21 @@ __global__ __launch_bounds__(kThreads, D >= 128 ? 1 : 2) void fwd_f32_kernel(Fwd
       for (int s = 0; s < D / 2; ++s)
         st[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kbuf[(2 * s + h) * kBN + 32 * t + r], qf[s], st[t], 0, 0, 0);
     }
-    if ((POL != 0 && cls == 1) || k0 + kBN > nk) {
+    if (cls == 1) {
+      const int base = k0 + 4 * h - klo;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int key = k0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
-          bool ok = key < nk;
-          if (POL != 0) ok &= check_orders_bf(a.rule, qo, seq_order(a.rule.k, a.rule, key)) | (cls == 2);
+          const int off = 32 * t + (i & 3) + 8 * (i >> 2);
+          bool ok;
+          if (POL == 1) {
+            ok = (unsigned)(base + off) < (unsigned)kspan;
+          } else {
+            const int key = k0 + off + 4 * h;
+            ok = key < nk;
+            if (POL == 2) ok &= check_orders_bf(a.rule, qo, seq_order(a.rule.k, a.rule, key));
+          }
           st[t][i] = ok ? st[t][i] : kNegInf;
         }
     }
@@ -258,7 +283,8 @@ template <int D>
 hipError_t launch_t(const FwdArgs& a, hipStream_t s) {
   const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
   const int smem = Smem32<D>::kTotal;
-  auto kern = a.rule.policy == 0 ? fwd_f32_kernel<D, 0> : fwd_f32_kernel<D, 1>;
+  const int pol = a.rule.policy == 0 ? 0 : (rule_is_interval(a.rule) ? 1 : 2);
+  auto kern = pol == 0 ? fwd_f32_kernel<D, 0> : (pol == 1 ? fwd_f32_kernel<D, 1> : fwd_f32_kernel<D, 2>);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      smem);
   if (e != hipSuccess) return e;

@@ -159,6 +159,28 @@ FA_HD void q_range_for_k_block(const Rule& r, int32_t k0, int32_t k1, int32_t* q
   if (*qe < *qb) *qe = *qb;
 }
 
+// Rules under which the keys allowed for one query form a contiguous INDEX
+// interval: full, causal (any dims: orders are monotone in the index), and 1d
+// local with unit stride (|dq - dk| < ws, plus qo >= ko when causal).
+FA_HD bool rule_is_interval(const Rule& r) {
+  return r.policy != 2 || (r.seq_dims == 1 && r.ls == 0);
+}
+
+// Inclusive key-index interval [*klo, *khi] allowed for query index qi under an
+// interval rule (*khi < *klo when empty).  Both bounds are non-decreasing in qi.
+FA_HD void key_interval(const Rule& r, int32_t qi, int32_t* klo, int32_t* khi) {
+  const int32_t nk = r.k.n;
+  if (r.policy == 0) { *klo = 0; *khi = nk - 1; return; }
+  const int32_t qo = seq_order(r.q, r, qi);
+  int32_t ohi = qo;  // causal: ko <= qo
+  *klo = 0;
+  if (r.policy == 2) {  // 1d: coordinate == order; |qo - ko| <= ws - 1
+    if (r.look_ahead != 1) ohi = qo + (r.ws - 1);
+    *klo = lower_bound_order(r.k, r, qo - (r.ws - 1));
+  }
+  *khi = lower_bound_order(r.k, r, ohi + 1) - 1;
+}
+
 // Tile classification for Q rows [q0, q1] x K cols [k0, k1] (all indices valid):
 //   2 = every pair allowed (no per-element check needed),
 //   1 = mixed (per-element check), 0 = no pair allowed.
