@@ -480,6 +480,8 @@ bool fwd_f16_supported(const FwdArgs& a) {
 hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s) {
   const int dm = max(a.d, a.v_d);
   const int v = env_variant();
+  // FA_FWD_VARIANT < 1000 pins the general kernel (A/B runs); otherwise the streamlined one takes its shapes
+  if ((v < 0 || v >= 1000) && fwd_f16_fast_supported(a)) return launch_fwd_f16_fast(a, s);
   if (dm <= 32) return launch_t<32, 4, 8>(a, s);
   if (dm <= 64) {
     switch (v) {
