@@ -198,6 +198,22 @@ def test_f16_mfma_shapes(d, policy, nq, nk):
     run_case(np.float16, policy, 1, "none_front", (2, 2), d, d, (nq,), (nk,), ws=33, ls=0, causal=False, seed=d)
 
 
+# fp16 streamlined forward / two-pass backward (d in {64, 128}, nq % 8 == nk % 8 == 0): ragged
+# last tiles on both axes, every interval rule, sync maps, and 2d causal orders
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("policy,ws,causal,seq_dims,mode,qs,ks", [
+    ("full", 1, False, 1, "none_front", (264,), (136,)),
+    ("causal", 1, False, 1, "none_front", (392,), (392,)),
+    ("causal", 1, False, 1, "scale_end", (200,), (520,)),
+    ("local", 33, False, 1, "none_front", (456,), (456,)),
+    ("local", 70, True, 1, "scale_front", (240,), (480,)),
+    ("causal", 1, False, 2, "scale_front", (8, 24), (16, 16)),
+    ("full", 1, False, 2, "none_front", (16, 16), (8, 40)),
+])
+def test_f16_fast_paths(d, policy, ws, causal, seq_dims, mode, qs, ks):
+    run_case(np.float16, policy, seq_dims, mode, (2, 2), d, d, qs, ks, ws=ws, ls=0, causal=causal, seed=d + ws)
+
+
 @pytest.mark.parametrize("d", [16, 32, 48, 64, 96, 128])
 @pytest.mark.parametrize("policy", ["full", "causal", "local"])
 @pytest.mark.parametrize("nq,nk", [(256, 256), (130, 1001)])

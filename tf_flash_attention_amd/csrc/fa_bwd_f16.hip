@@ -18,6 +18,8 @@
 #include "fa_device.h"
 #include "fa_kernels.h"
 
+#include <stdlib.h>
+
 namespace fa {
 namespace {
 
@@ -356,6 +358,10 @@ bool bwd_f16_supported(const BwdArgs& a) {
 }
 
 hipError_t launch_bwd_f16(const BwdArgs& a, hipStream_t s) {
+  // FA_BWD_VARIANT=0 pins this single-pass atomic kernel (A/B runs); otherwise the two-pass
+  // kernels take the shapes they support
+  const char* ev = getenv("FA_BWD_VARIANT");
+  if (!(ev && atoi(ev) == 0) && bwd_f16_fast_supported(a)) return launch_bwd_f16_fast(a, s);
   const int nq = a.rule.q.n;
   hipError_t e = hipMemsetAsync(a.ws_dQ, 0, sizeof(float) * (size_t)a.b * a.d * nq, s);
   if (e != hipSuccess) return e;

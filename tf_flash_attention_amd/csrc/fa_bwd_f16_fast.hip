@@ -1,0 +1,598 @@
+// fa_bwd_f16_fast.hip — fp16 fused attention backward on gfx950 MFMA for the
+// common shapes (d == v_d ∈ {64, 128}, 16-byte aligned rows, nq % 8 == nk % 8 == 0)
+// under the full policy and the interval rules (causal, 1d unit-stride local).
+//
+// Replaces the reference's BackwardImpl (flash_attention.cu:1079-1967), which ran
+// every (key block, query block) pair as scalar SIMT GEMMs and serialised the dQ
+// read-modify-write through a global spin lock.  Here the pass is split the way
+// the data wants to flow on this chip — no atomics, no locks, no dQ workspace:
+//   prep : D = rowsum(dO∘O), lse2 = m·log2e + log2 l                (per query)
+//   dkdv : key-outer.  A wave owns 32 keys; K·scale·log2e and V stay in registers
+//          as MFMA B operands, dK and dV accumulate in registers, and the query
+//          tiles (Q, dO, lse2, D) stream through a 2-slot LDS ring:
+//              S  = Qᵀ·K'  (C = -lse2)   P  = exp2(S)
+//              dP = dOᵀ·V  (C = -D)      dS = P∘dP
+//              dV += dO·P,  dK += Q·dS   (P, dS straight from the accumulators)
+//   dq   : query-outer, the forward's structure.  A wave owns 32 queries; Q' and
+//          dO stay in registers as B operands and the key tiles stream through LDS:
+//              Sᵀ = Kᵀ·Q' (C = -lse2)    dPᵀ = Vᵀ·dO (C = -D)
+//              dQ += K·(Pᵀ∘dPᵀ)
+// The dq pass recomputes Sᵀ and dPᵀ (4d of the 14d MFMA FLOPs per allowed pair
+// against the algorithmic 10d) in exchange for writing dQ exactly once; the
+// single-kernel alternative (fa_bwd_f16.hip) spends that in fp32 atomics, which
+// cap it at ≈ 1.3 TB/s of added bytes (MI355X_MICROARCH.md 'Global float atomics').
+// Masks are rules (fa_rules.h): per-lane index intervals and per-wave tile classes;
+// tiles with no allowed pair are skipped.
+#include "fa_device.h"
+#include "fa_kernels.h"
+#include "fa_mfma.h"
+
+#include <stdlib.h>
+
+namespace fa {
+namespace {
+
+using namespace mf;
+
+constexpr int kThrPrep = 256;
+
+// ---------------------------------------------------------------------------
+// prep: D = rowsum(dO∘O) (fp32), lse2 = m*log2e + log2(l) (+inf if the row attends nothing)
+__global__ __launch_bounds__(kThrPrep) void bwd_prep_kernel(BwdArgs a) {
+  const int nq = a.rule.q.n, vd = a.v_d;
+  const int64_t total = a.b * (int64_t)nq;
+  const int64_t i = blockIdx.x * (int64_t)kThrPrep + threadIdx.x;
+  if (i >= total) return;
+  const int64_t bi = i / nq;
+  const int q = (int)(i - bi * nq);
+  const __half* O = static_cast<const __half*>(a.O) + bi * (int64_t)vd * nq + q;
+  const __half* dO = static_cast<const __half*>(a.dO) + bi * (int64_t)vd * nq + q;
+  float D0 = 0.f, D1 = 0.f;
+  int v = 0;
+  for (; v + 1 < vd; v += 2) {
+    D0 += __half2float(O[(int64_t)v * nq]) * __half2float(dO[(int64_t)v * nq]);
+    D1 += __half2float(O[(int64_t)(v + 1) * nq]) * __half2float(dO[(int64_t)(v + 1) * nq]);
+  }
+  if (v < vd) D0 += __half2float(O[(int64_t)v * nq]) * __half2float(dO[(int64_t)v * nq]);
+  const float l = static_cast<const float*>(a.l)[i];
+  const float m = __half2float(static_cast<const __half*>(a.m)[i]);
+  static_cast<float*>(a.ws_D)[i] = D0 + D1;
+  static_cast<float*>(a.ws_lse)[i] = (l > 0.f) ? m * kLog2e + __log2f(l) : __builtin_huge_valf();
+}
+
+// ---------------------------------------------------------------------------
+// LDS images
+//   "row image"  [D][W] fp16, W = 32*NW columns, 16-B chunks XOR-swizzled by (row & 3) << 6
+//                (B-operand transposed reads conflict-free; the forward's Q tile)
+//   "KT image"   [D][64] fp16, 128-B rows, 64-B halves swapped on rows with c&2
+//                (A operand Kᵀ / Vᵀ of a 64-key tile by transposed reads)
+//   "G image"    [2*nb groups][D+1][8] fp16: group (s, h) holds columns
+//                {16s + 4h + 0..3, 16s + 8 + 4h + 0..3} of each row, so one ds_read_b128
+//                is the A operand whose k order matches a 32x32 accumulator's register
+//                order (P / dS used as B operands without any shuffle)
+//   "QT image"   [D][32] fp16, 64-B rows, 8-B chunks XOR-swizzled by row>>2
+//                (A operand Qᵀ / dOᵀ of a 32-query tile by transposed reads)
+constexpr int kGPad = 1;  // G image rows of padding (16 B) per group
+
+__device__ __forceinline__ uint32_t qt_off(int row, int col) {  // col multiple of 4
+  return row * 64 + ((((col >> 2) ^ (row >> 2)) & 7) << 3);
+}
+__device__ __forceinline__ uint32_t kt_off(int row, int col) {  // col multiple of 4 (or 8)
+  return row * 128 + ((col * 2) ^ ((row & 2) << 5));
+}
+template <int D>
+__device__ __forceinline__ uint32_t g_off(int s, int h, int row) {
+  return ((2 * s + h) * (D + kGPad) + row) * 16;
+}
+// chunk m (8 consecutive columns 8m..8m+7) of row c -> two 8-B halves of the G image
+template <int D>
+__device__ __forceinline__ void g_store(lds_char_t* img, int c, int m, u32x4 v) {
+  lds_char_t* p = img + g_off<D>(m >> 1, 0, c) + (m & 1) * 8;
+  *reinterpret_cast<lds_u32x2_t*>(p) = v.xy;
+  *reinterpret_cast<lds_u32x2_t*>(p + (D + kGPad) * 16) = v.zw;
+}
+
+template <int D, int NW>
+struct DkdvSmem {
+  static constexpr int kBK = 32 * NW;                 // keys per workgroup
+  static constexpr int kRow = D * kBK * 2;            // K (or V) row image
+  static constexpr int kQT = D * 64;                  // one [D][32] QT image
+  static constexpr int kG = 4 * (D + kGPad) * 16;     // one 32-column G image
+  static constexpr int offQT = 0, offOT = kQT, offQG = 2 * kQT, offOG = 2 * kQT + kG, offLse = 2 * kQT + 2 * kG;
+  static constexpr int kSlot = offLse + 2 * 32 * 4;   // + lse2[32], D[32]
+  static constexpr int kRing = 2 * kSlot;
+  static constexpr int kTotal = (kRing > 2 * kRow) ? kRing : 2 * kRow;  // the K/V images alias the ring
+};
+
+// ---------------------------------------------------------------------------
+// dK / dV: key-outer.  One workgroup = NW waves x 32 keys of one (batch, head) slice.
+template <int D, int NW, int WPE, int POL>
+__global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char_t* smem = (lds_char_t*)smem_raw;
+  using S = DkdvSmem<D, NW>;
+  constexpr int kThr = NW * 64;
+  constexpr int kBK = S::kBK;
+  constexpr int kQChunks = D * 4;                     // 16-B chunks of one [D][32] tile
+  static_assert((2 * kQChunks) % kThr == 0, "tile chunks must divide over the workgroup");
+  constexpr int kCPT = 2 * kQChunks / kThr;           // Q and dO chunks per thread
+
+  const int nq = a.rule.q.n, nk = a.rule.k.n;
+  const uint32_t nkb = (nk + kBK - 1) / kBK;
+  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t bi = bid / nkb;
+  const int k0 = (int)(bid % nkb) * kBK;  // earliest (heaviest under causal) key blocks first
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, r = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const float c2 = (float)a.scale * kLog2e;
+
+  const __half* K = static_cast<const __half*>(a.K) + bi * (int64_t)D * nk;
+  const __half* V = static_cast<const __half*>(a.V) + bi * (int64_t)D * nk;
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(static_cast<const __half*>(a.Q) + bi * (int64_t)D * nq, 2u * D * nq);
+  const __amdgpu_buffer_rsrc_t ors = make_rsrc(static_cast<const __half*>(a.dO) + bi * (int64_t)D * nq, 2u * D * nq);
+  const float* glse = static_cast<const float*>(a.ws_lse) + bi * (int64_t)nq;
+  const float* gD = static_cast<const float*>(a.ws_D) + bi * (int64_t)nq;
+
+  // ---- resident B operands: lane (r,h) holds X[c = 16s + 8h + j][key = k0 + 32w + r]
+  half8 kb[D / 16], vb[D / 16];
+  {
+    for (int idx = tid; idx < 2 * D * (kBK / 8); idx += kThr) {
+      const int which = idx >= D * (kBK / 8);
+      const int j = which ? idx - D * (kBK / 8) : idx;
+      const int c = j / (kBK / 8), m = j % (kBK / 8);
+      const u32x4 v = load_chunk8((which ? V : K) + (int64_t)c * nk, k0 + 8 * m, nk, true);
+      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBK) + ((m * 16) ^ ((c & 3) << 6))) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int crow = 16 * s + 8 * (g >> 1) + 4 * e + tq;
+        const int col = 32 * w + 16 * (g & 1) + 4 * tp;
+        const uint32_t off = crow * (2 * kBK) + ((col * 2) ^ ((crow & 3) << 6));
+        const half4 x = tr_read(smem + off), y = tr_read(smem + S::kRow + off);
+        if (e == 0) { kb[s].lo = x; vb[s].lo = y; } else { kb[s].hi = x; vb[s].hi = y; }
+      }
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) kb[s] = scale8(kb[s], c2);  // S in log2 units straight out of the MFMA
+    __syncthreads();  // the K/V images are reused by the ring
+  }
+
+  // ---- query range of this key block and the per-lane / per-wave query intervals
+  const int klast = min(k0 + kBK, nk) - 1;
+  int qb = 0, qe = nq;
+  if (POL != 0) q_range_for_k_block(a.rule, k0, klast, &qb, &qe);
+  const int qt0 = (qb / 32) * 32;
+  const int ntiles = (qe > qb) ? (qe - qt0 + 31) / 32 : 0;
+  const int key = k0 + 32 * w + r;
+  const int wk0 = k0 + 32 * w;
+  const bool wave_active = wk0 < nk;
+  int qlo = 0, qspan = nq, wlo_min = 0, wlo_max = 0, whi_min = nq - 1, whi_max = nq - 1;
+  if (POL == 1 && wave_active) {
+    int qhi;
+    query_interval(a.rule, min(key, nk - 1), &qlo, &qhi);
+    qspan = max(qhi - qlo + 1, 0);
+    const int last = min(31, nk - 1 - wk0);
+    wlo_min = __builtin_amdgcn_readfirstlane(qlo);
+    whi_min = __builtin_amdgcn_readfirstlane(qhi);
+    wlo_max = __builtin_amdgcn_readlane(qlo, last);
+    whi_max = __builtin_amdgcn_readlane(qhi, last);
+  }
+  // 0: no allowed pair for this wave, 1: mixed (per-element mask), 2: all allowed
+  auto tcls = [&](int qa) -> int {
+    const int qz = qa + 31;
+    if (!wave_active) return 0;
+    if (POL == 0) return 2;  // q >= nq rows carry lse2 = +inf -> P = 0; keys >= nk are never stored
+    if (wlo_min > qz || whi_max < qa) return 0;
+    return (wlo_max <= qa && whi_min >= qz) ? 2 : 1;
+  };
+
+  // ---- query-tile staging (Q, dO chunks: 8 queries of one channel row)
+  uint32_t voff[kCPT];
+  int crow_[kCPT], cm_[kCPT];
+#pragma unroll
+  for (int j = 0; j < kCPT; ++j) {
+    const int idx = (tid + kThr * j) % kQChunks;
+    crow_[j] = idx >> 2;
+    cm_[j] = idx & 3;
+    voff[j] = (uint32_t)crow_[j] * (uint32_t)nq * 2u + 16u * cm_[j];
+  }
+  u32x4 qr[kCPT];
+  float lr = 0.f;
+  // chunk j holds dO (else Q); compile-time when the chunks divide evenly over the threads
+  auto is_o = [&](int j) -> bool {
+    return (kQChunks % kThr == 0) ? (j >= kQChunks / kThr) : ((tid + kThr * j) >= kQChunks);
+  };
+  auto load_tile = [&](int qa) {
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isO = is_o(j);
+      const bool out = qa + 8 * cm_[j] >= nq;
+      qr[j] = buf_load16(isO ? ors : qrs, voff[j], 2 * qa, out);
+    }
+    if (tid < 64) {  // lanes 0..31: lse2, 32..63: D
+      const int q = qa + (tid & 31);
+      lr = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? __builtin_huge_valf() : 0.f);
+    }
+  };
+  auto store_tile = [&](int slot) {
+    lds_char_t* base = smem + slot * S::kSlot;
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isO = is_o(j);
+      lds_char_t* t = base + (isO ? S::offOT : S::offQT);
+      lds_char_t* gi = base + (isO ? S::offOG : S::offQG);
+      *reinterpret_cast<lds_u32x2_t*>(t + qt_off(crow_[j], 8 * cm_[j])) = qr[j].xy;
+      *reinterpret_cast<lds_u32x2_t*>(t + qt_off(crow_[j], 8 * cm_[j] + 4)) = qr[j].zw;
+      g_store<D>(gi, crow_[j], cm_[j], qr[j]);
+    }
+    if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr;
+  };
+
+  floatx16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { dk[u][i] = 0.f; dv[u][i] = 0.f; }
+
+  if (ntiles > 0) { load_tile(qt0); store_tile(0); }
+  if (ntiles > 1) load_tile(qt0 + 32);
+
+  // iteration it: tile it in slot it&1 (complete after the barrier); tile it+1 -> slot (it+1)&1
+  // (read in iteration it-1, finished before this barrier); tile it+2 -> registers
+  auto step = [&](auto P_, int it) {
+    constexpr int p = decltype(P_)::value;
+    __syncthreads();
+    const int qa = qt0 + 32 * it;
+    if (it + 1 < ntiles) store_tile(p ^ 1);
+    if (it + 2 < ntiles) load_tile(qa + 64);
+    const int cls = tcls(qa);
+    if (cls == 0) return;
+    const lds_char_t* base = smem + p * S::kSlot;
+    // row constants as the initial accumulators: S: -lse2[q], dP: -D[q], q = (i&3) + 8(i>>2) + 4h
+    floatx16 sacc, pacc;
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const floatx4 l4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 4 * (8 * gq + 4 * h));
+      const floatx4 d4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 128 + 4 * (8 * gq + 4 * h));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sacc[4 * gq + j] = -l4[j];
+        pacc[4 * gq + j] = -d4[j];
+      }
+    }
+    // S = Qᵀ·K', dP = dOᵀ·V: A operands (row q, k = channel) by transposed reads
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      half8 qa8, oa8;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const uint32_t off = qt_off(16 * s + 8 * (g >> 1) + 4 * e + tq, 16 * (g & 1) + 4 * tp);
+        const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
+        if (e == 0) { qa8.lo = x; oa8.lo = y; } else { qa8.hi = x; oa8.hi = y; }
+      }
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8, kb[s], sacc, 0, 0, 0);
+      pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8, vb[s], pacc, 0, 0, 0);
+    }
+    // P = exp2(S), dS = P∘dP; k-step s of the dV / dK products = registers 8s..8s+7
+    half8 pf[2], sf[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float pv = __builtin_amdgcn_exp2f(sacc[i]);
+      if (POL == 1 && cls == 1) {
+        const int q = qa + (i & 3) + 8 * (i >> 2) + 4 * h;
+        pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
+      }
+      pf[i >> 3][i & 7] = (_Float16)pv;
+      sf[i >> 3][i & 7] = (_Float16)(pv * pacc[i]);
+    }
+    // dV += dO·P, dK += Q·dS: A = X[row 32u + r][group (s, h)] (G images)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int u = 0; u < D / 32; ++u) {
+        const half8 oa = read_b128(base + S::offOG + g_off<D>(s, h, 32 * u + r));
+        const half8 qa = read_b128(base + S::offQG + g_off<D>(s, h, 32 * u + r));
+        dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa, pf[s], dv[u], 0, 0, 0);
+        dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa, sf[s], dk[u], 0, 0, 0);
+      }
+  };
+  for (int it = 0; it < ntiles; it += 2) {
+    step(IC<0>{}, it);
+    if (it + 1 < ntiles) step(IC<1>{}, it + 1);
+  }
+
+  // ---- dK = scale·Σ dS·Q, dV: rows c = 32u + (i&3) + 8(i>>2) + 4h, column = this lane's key
+  if (!wave_active || key >= nk) return;
+  __half* dK = static_cast<__half*>(a.dK) + bi * (int64_t)D * nk;
+  __half* dV = static_cast<__half*>(a.dV) + bi * (int64_t)D * nk;
+  const float sc = (float)a.scale;
+#pragma unroll
+  for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+      dK[(int64_t)c * nk + key] = __float2half(dk[u][i] * sc);
+      dV[(int64_t)c * nk + key] = __float2half(dv[u][i]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+template <int D, int NW>
+struct DqSmem {
+  static constexpr int kBM = 32 * NW;                 // queries per workgroup
+  static constexpr int kRow = D * kBM * 2;            // Q (or dO) row image
+  static constexpr int kKT = D * 128;                 // one [D][64] KT image
+  static constexpr int kG = 8 * (D + kGPad) * 16;     // one 64-column G image
+  static constexpr int offKT = 0, offVT = kKT, offKG = 2 * kKT;
+  static constexpr int kSlot = 2 * kKT + kG;
+  static constexpr int kRing = 2 * kSlot;
+  static constexpr int kTotal = (kRing > 2 * kRow) ? kRing : 2 * kRow;  // the Q/dO images alias the ring
+};
+
+// dQ: query-outer.  One workgroup = NW waves x 32 queries of one (batch, head) slice.
+template <int D, int NW, int WPE, int POL>
+__global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char_t* smem = (lds_char_t*)smem_raw;
+  using S = DqSmem<D, NW>;
+  constexpr int kThr = NW * 64;
+  constexpr int kBM = S::kBM;
+  constexpr int kBN = 64;
+  constexpr int kKChunks = D * 8;                     // 16-B chunks of one [D][64] tile
+  static_assert((2 * kKChunks) % kThr == 0, "tile chunks must divide over the workgroup");
+  constexpr int kCPT = 2 * kKChunks / kThr;           // K and V chunks per thread
+  constexpr float kNegInf = -__builtin_huge_valf();
+
+  const int nq = a.rule.q.n, nk = a.rule.k.n;
+  const uint32_t nqb = (nq + kBM - 1) / kBM;
+  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t bi = bid / nqb;
+  const int q0 = (int)(nqb - 1 - (bid % nqb)) * kBM;  // latest (heaviest under causal) blocks first
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, r = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const float c2 = (float)a.scale * kLog2e;
+
+  const __half* Q = static_cast<const __half*>(a.Q) + bi * (int64_t)D * nq;
+  const __half* dO = static_cast<const __half*>(a.dO) + bi * (int64_t)D * nq;
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + bi * (int64_t)D * nk, 2u * D * nk);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + bi * (int64_t)D * nk, 2u * D * nk);
+
+  const int wq0 = q0 + 32 * w;
+  const int qi = wq0 + r;
+  const bool wave_active = wq0 < nq;
+
+  // ---- resident B operands: lane (r,h) holds X[c = 16s + 8h + j][q = wq0 + r]
+  half8 qf[D / 16], of[D / 16];
+  {
+    for (int idx = tid; idx < 2 * D * (kBM / 8); idx += kThr) {
+      const int which = idx >= D * (kBM / 8);
+      const int j = which ? idx - D * (kBM / 8) : idx;
+      const int c = j / (kBM / 8), m = j % (kBM / 8);
+      const u32x4 v = load_chunk8((which ? dO : Q) + (int64_t)c * nq, q0 + 8 * m, nq, true);
+      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBM) + ((m * 16) ^ ((c & 3) << 6))) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int crow = 16 * s + 8 * (g >> 1) + 4 * e + tq;
+        const int col = 32 * w + 16 * (g & 1) + 4 * tp;
+        const uint32_t off = crow * (2 * kBM) + ((col * 2) ^ ((crow & 3) << 6));
+        const half4 x = tr_read(smem + off), y = tr_read(smem + S::kRow + off);
+        if (e == 0) { qf[s].lo = x; of[s].lo = y; } else { qf[s].hi = x; of[s].hi = y; }
+      }
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) qf[s] = scale8(qf[s], c2);
+    __syncthreads();  // the Q/dO images are reused by the ring
+  }
+  // row constants (this lane's query) as the C operands of the Sᵀ / dPᵀ chains
+  floatx16 negl, negd;
+  {
+    const float* glse = static_cast<const float*>(a.ws_lse) + bi * (int64_t)nq;
+    const float* gD = static_cast<const float*>(a.ws_D) + bi * (int64_t)nq;
+    const float lv = (qi < nq) ? -glse[qi] : kNegInf, dv = (qi < nq) ? -gD[qi] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { negl[i] = lv; negd[i] = dv; }
+  }
+
+  // ---- key range of this query block (rule-bounded), per-lane key intervals
+  const int qlast = min(q0 + kBM, nq) - 1;
+  int kb = 0, ke = nk;
+  if (POL != 0) k_range_for_q_block(a.rule, q0, qlast, &kb, &ke);
+  const int kt0 = (kb / kBN) * kBN;
+  const int ntiles = (ke > kb) ? (ke - kt0 + kBN - 1) / kBN : 0;
+  int klo = 0, kspan = nk, wlo_min = 0, wlo_max = 0, whi_min = nk - 1, whi_max = nk - 1;
+  if (POL == 1 && wave_active) {
+    int khi;
+    key_interval(a.rule, min(qi, nq - 1), &klo, &khi);
+    kspan = max(khi - klo + 1, 0);
+    const int last = min(31, nq - 1 - wq0);
+    wlo_min = __builtin_amdgcn_readfirstlane(klo);
+    whi_min = __builtin_amdgcn_readfirstlane(khi);
+    wlo_max = __builtin_amdgcn_readlane(klo, last);
+    whi_max = __builtin_amdgcn_readlane(khi, last);
+  }
+  auto tcls = [&](int ka) -> int {
+    const int kz = ka + kBN - 1;
+    if (!wave_active) return 0;
+    if (POL == 0) return kz < nk ? 2 : 1;
+    if (wlo_min > kz || whi_max < ka) return 0;
+    return (wlo_max <= ka && whi_min >= kz && kz < nk) ? 2 : 1;
+  };
+
+  // ---- key-tile staging (K, V chunks: 8 keys of one channel row)
+  uint32_t voff[kCPT];
+  int crow_[kCPT];
+  const int cm = tid & 7;
+#pragma unroll
+  for (int j = 0; j < kCPT; ++j) {
+    crow_[j] = ((tid + kThr * j) % kKChunks) >> 3;
+    voff[j] = (uint32_t)crow_[j] * (uint32_t)nk * 2u + 16u * cm;
+  }
+  u32x4 kr[kCPT];
+  auto is_v = [&](int j) -> bool {
+    return (kKChunks % kThr == 0) ? (j >= kKChunks / kThr) : ((tid + kThr * j) >= kKChunks);
+  };
+  auto load_tile = [&](int ka) {
+    const bool out = ka + 8 * cm >= nk;
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isV = is_v(j);
+      kr[j] = buf_load16(isV ? vrs : krs, voff[j], 2 * ka, out);
+    }
+  };
+  auto store_tile = [&](int slot) {
+    lds_char_t* base = smem + slot * S::kSlot;
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isV = is_v(j);
+      *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + kt_off(crow_[j], 8 * cm)) = kr[j];
+      if (!isV) g_store<D>(base + S::offKG, crow_[j], cm, kr[j]);
+    }
+  };
+
+  floatx16 dq[D / 32];
+#pragma unroll
+  for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[u][i] = 0.f;
+
+  // A-operand (Kᵀ / Vᵀ) read bases: element (crow, col) of a KT image
+  const uint32_t tb0 = kt_off(8 * (g >> 1) + tq, 16 * (g & 1) + 4 * tp);
+  const uint32_t tb1 = kt_off(8 * (g >> 1) + tq, 32 + 16 * (g & 1) + 4 * tp);
+
+  if (ntiles > 0) { load_tile(kt0); store_tile(0); }
+  if (ntiles > 1) load_tile(kt0 + kBN);
+
+  auto step = [&](auto P_, int it) {
+    constexpr int p = decltype(P_)::value;
+    __syncthreads();
+    const int ka = kt0 + it * kBN;
+    if (it + 1 < ntiles) store_tile(p ^ 1);
+    if (it + 2 < ntiles) load_tile(ka + 2 * kBN);
+    const int cls = tcls(ka);
+    if (cls == 0) return;
+    const lds_char_t* base = smem + p * S::kSlot;
+    floatx16 st[2], dp[2];
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        half8 kf, vf;
+        const uint32_t b = (t ? tb1 : tb0) + (16 * s) * 128;
+        kf.lo = tr_read(base + S::offKT + b);
+        kf.hi = tr_read(base + S::offKT + b + 4 * 128);
+        vf.lo = tr_read(base + S::offVT + b);
+        vf.hi = tr_read(base + S::offVT + b + 4 * 128);
+        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], s == 0 ? negl : st[t], 0, 0, 0);
+        dp[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, of[s], s == 0 ? negd : dp[t], 0, 0, 0);
+      }
+    // dSᵀ = exp2(Sᵀ)∘dPᵀ; keys of register i of half t: 32t + (i&3) + 8(i>>2) + 4h
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      half8 dsf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = s >> 1, i = 8 * (s & 1) + j;
+        float pv = __builtin_amdgcn_exp2f(st[t][i]);
+        if (cls == 1) {
+          const int kk = ka + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+          const bool ok = (POL == 1) ? ((unsigned)(kk - klo) < (unsigned)kspan) : (kk < nk);
+          pv = ok ? pv : 0.f;
+        }
+        dsf[j] = (_Float16)(pv * dp[t][i]);
+      }
+#pragma unroll
+      for (int u = 0; u < D / 32; ++u) {
+        const half8 ka8 = read_b128(base + S::offKG + g_off<D>(s, h, 32 * u + r));
+        dq[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka8, dsf, dq[u], 0, 0, 0);
+      }
+    }
+  };
+  for (int it = 0; it < ntiles; it += 2) {
+    step(IC<0>{}, it);
+    if (it + 1 < ntiles) step(IC<1>{}, it + 1);
+  }
+
+  if (!wave_active || qi >= nq) return;
+  __half* dQ = static_cast<__half*>(a.dQ) + bi * (int64_t)D * nq;
+  const float sc = (float)a.scale;
+#pragma unroll
+  for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+      dQ[(int64_t)c * nq + qi] = __float2half(dq[u][i] * sc);
+    }
+}
+
+template <int D, int NW, int WPE>
+hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
+  using S = DkdvSmem<D, NW>;
+  const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
+  auto kern = a.rule.policy == 0 ? bwd_dkdv_kernel<D, NW, WPE, 0> : bwd_dkdv_kernel<D, NW, WPE, 1>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     S::kTotal);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(NW * 64), S::kTotal, s, a);
+  return hipGetLastError();
+}
+
+template <int D, int NW, int WPE>
+hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
+  using S = DqSmem<D, NW>;
+  const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
+  auto kern = a.rule.policy == 0 ? bwd_dq_kernel<D, NW, WPE, 0> : bwd_dq_kernel<D, NW, WPE, 1>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     S::kTotal);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(NW * 64), S::kTotal, s, a);
+  return hipGetLastError();
+}
+
+int bwd_variant() {
+  const char* e = getenv("FA_BWD_VARIANT");
+  return e ? atoi(e) : -1;
+}
+
+}  // namespace
+
+bool bwd_f16_fast_supported(const BwdArgs& a) {
+  const int nq = a.rule.q.n, nk = a.rule.k.n;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(a.Q) | reinterpret_cast<uintptr_t>(a.K) |
+                       reinterpret_cast<uintptr_t>(a.V) | reinterpret_cast<uintptr_t>(a.dO);
+  return a.d == a.v_d && (a.d == 64 || a.d == 128) && nq > 0 && nk > 0 && nq % 8 == 0 && nk % 8 == 0 &&
+         (al % 16) == 0 && (int64_t)a.d * nq * 2 < (1ll << 31) && (int64_t)a.d * nk * 2 < (1ll << 31) &&
+         rule_is_interval(a.rule) && a.b * ((nk + 127) / 128) < (1ll << 31) && a.b * ((nq + 127) / 128) < (1ll << 31);
+}
+
+hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
+  const int64_t nrows = a.b * (int64_t)a.rule.q.n;
+  hipLaunchKernelGGL(bwd_prep_kernel, dim3((unsigned)((nrows + kThrPrep - 1) / kThrPrep)), dim3(kThrPrep), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int v = bwd_variant();
+  if (a.d == 64) {
+    switch (v) {
+      case 82: e = launch_dkdv<64, 8, 2>(a, s); break;
+      default: e = launch_dkdv<64, 4, 2>(a, s); break;
+    }
+    if (e != hipSuccess) return e;
+    switch (v) {
+      case 82: return launch_dq<64, 8, 2>(a, s);
+      default: return launch_dq<64, 4, 2>(a, s);
+    }
+  }
+  e = launch_dkdv<128, 4, 1>(a, s);
+  if (e != hipSuccess) return e;
+  return launch_dq<128, 4, 1>(a, s);
+}
+
+}  // namespace fa

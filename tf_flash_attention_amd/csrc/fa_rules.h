@@ -181,6 +181,21 @@ FA_HD void key_interval(const Rule& r, int32_t qi, int32_t* klo, int32_t* khi) {
   *khi = lower_bound_order(r.k, r, ohi + 1) - 1;
 }
 
+// Inclusive query-index interval [*qlo, *qhi] allowed for key index ki under an
+// interval rule (*qhi < *qlo when empty) — the transpose of key_interval, used by
+// the key-outer backward.  Both bounds are non-decreasing in ki.
+FA_HD void query_interval(const Rule& r, int32_t ki, int32_t* qlo, int32_t* qhi) {
+  const int32_t nq = r.q.n;
+  if (r.policy == 0) { *qlo = 0; *qhi = nq - 1; return; }
+  const int32_t ko = seq_order(r.k, r, ki);
+  *qlo = lower_bound_order(r.q, r, ko);  // causal (and causal-local): qo >= ko
+  *qhi = nq - 1;
+  if (r.policy == 2) {  // 1d: |qo - ko| <= ws - 1
+    if (r.look_ahead != 1) *qlo = lower_bound_order(r.q, r, ko - (r.ws - 1));
+    *qhi = lower_bound_order(r.q, r, ko + r.ws) - 1;
+  }
+}
+
 // Tile classification for Q rows [q0, q1] x K cols [k0, k1] (all indices valid):
 //   2 = every pair allowed (no per-element check needed),
 //   1 = mixed (per-element check), 0 = no pair allowed.
