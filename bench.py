@@ -128,8 +128,9 @@ def load_traffic(workload_key: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=50)
+    # the first ~20 launches on a fresh box run ~15 % slow (clock ramp); 40 untimed steps cover it
+    ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")

@@ -5,16 +5,17 @@
 // Same algorithm and operand layouts as fa_fwd_f16.hip (which remains the path
 // for every other shape and for strided / 2d local rules); what differs is how
 // the key loop is laid out for the gfx950 issue port:
-//   * K and V have separate 2-slot LDS rings.  Iteration `it` reads K(it+1) (for
-//     the Sᵀ MFMAs of the next tile) and V(it) (for this tile's PV MFMAs), and
-//     writes K(it+2) / V(it+1) into the slots the previous iteration finished
-//     with — one barrier per key tile, and the loop unrolled by two so every
-//     LDS address is a lane constant plus an immediate;
+//   * K and V have separate LDS rings of 2·TPB tiles, filled TPB tiles per barrier
+//     (TPB = tiles per barrier).  Tile `it` reads K(it+1) (for the Sᵀ MFMAs of the
+//     next tile) and V(it) (for its own PV MFMAs); each barrier phase writes the
+//     K and V tiles the previous phase finished with.  The loop is unrolled over
+//     the ring so every LDS address is a lane constant plus an immediate;
 //   * K/V tiles are fetched with buffer loads (one SGPR descriptor per slice,
 //     the tile offset in soffset): no per-tile address VALU;
-//   * all K and V fragment reads of a tile are issued together right after the
-//     barrier, before any of the tile's VALU, so LDS latency overlaps the
-//     softmax instead of serialising the MFMAs behind it;
+//   * K fragments are read right after the barrier, V fragments after the
+//     rebase decision (LDS latency overlaps the Sᵀ MFMAs / the row max);
+//   * the Sᵀ MFMAs of tile it+1 share a basic block with the row max of tile it;
+//     the exponentials of tile it interleave with its PV MFMAs;
 //   * full tiles take a branch-free path; only mixed tiles (rule edge / nk tail)
 //     evaluate a per-element mask.
 // Replaces the reference's ForwardImpl (flash_attention.cu:425-1077) for these
@@ -22,110 +23,54 @@
 // the stored fp16 m) are identical to fa_fwd_f16.hip.
 #include "fa_device.h"
 #include "fa_kernels.h"
+#include "fa_mfma.h"
 
 #include <stdlib.h>
 
 namespace fa {
 namespace {
 
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-typedef _Float16 half2v __attribute__((ext_vector_type(2)));
-typedef short v4i16 __attribute__((__vector_size__(8)));
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16_t;
-typedef __attribute__((address_space(3))) char lds_char_t;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
-typedef __attribute__((address_space(3))) u32x2 lds_u32x2_t;
+using namespace mf;
 
-constexpr int kBN = 64;      // keys per tile
-constexpr int kVPad = 1;     // V group row padding, in 16-byte rows
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLn2 = 0.6931471805599453f;
+constexpr int kBN = 64;             // keys per tile
+constexpr int kVPad = 1;            // V group row padding, in 16-byte rows
 constexpr float kRescaleThr = 8.f;  // log2 units (cdna_hip_programming.md T13)
 
 // structure flags (FA_FWD_VARIANT selects them for A/B timing; the launcher's default is tuned)
 constexpr int kFSumAdd = 1;  // row sums by f32 adds of the exponentials (else v_dot2 on packed P)
 constexpr int kFPrio = 2;    // s_setprio 1 for the second half of the waves (guide T5, static form)
 constexpr int kFLateV = 4;   // read the V fragments after the rebase decision (shorter live range)
-constexpr int kFOcc3 = 8;    // three waves per SIMD (<= 168 VGPRs)
-constexpr int kFDeep = 16;   // two register sets for the K/V staging: global loads two tiles ahead
+constexpr int kFTpb2 = 8;    // two key tiles per barrier (ring of 4 tiles for K and for V)
 // ablation bits: timing-only diagnostic builds (outputs are WRONG), FA_FWD_VARIANT=1899 + FA_FWD_ABL
-// kDiag: per-wave s_memtime sums of the loop phases written over the l output (diagnostic only)
-constexpr int kDiag = 4096;
 constexpr int kANoBar = 64, kANoExp = 128, kANoLoad = 256, kANoMax = 512, kANoQK = 1024, kANoPV = 2048;
 
-template <int D, int NW>
+template <int D, int NW, int TPB>
 struct FastSmem {
   static constexpr int kBM = 32 * NW;               // query rows per workgroup
   static constexpr int kQRow = 2 * kBM;             // bytes per Q row
   static constexpr int kQ = D * kQRow;              // Q [D][BM] halfs
   static constexpr int kK = D * kBN * 2;            // K tile [D][64] halfs, 128-B rows
   static constexpr int kV = 8 * (D + kVPad) * 16;   // V tile [8 groups][D+pad][8] halfs
-  static constexpr int offK = kQ;                   // K slots 0, 1
-  static constexpr int offV = kQ + 2 * kK;          // V slots 0, 1
-  static constexpr int kTotal = kQ + 2 * kK + 2 * kV;
+  static constexpr int kNS = 2 * TPB;               // ring slots (K and V each)
+  static constexpr int offK = kQ;
+  static constexpr int offV = kQ + kNS * kK;
+  static constexpr int kTotal = kQ + kNS * (kK + kV);
 };
 
-// max / sum of x over lanes l and l^32: after the half swap one result holds the
-// lower half twice and the other the upper half twice, so a symmetric op of the
-// two needs no lane select.
-__device__ __forceinline__ float max_pair32(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float sum_pair32(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
+constexpr int fast_waves_per_eu(int D) { return D >= 128 ? 1 : 2; }
 
-__device__ __forceinline__ half4 tr_read(const lds_char_t* p) {
-  const v4i16 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t*)p);
-  return __builtin_bit_cast(half4, t);
-}
-
-__device__ __forceinline__ u32x4 load_chunk_q(const __half* row, int e, int n, bool vec) {
-  if (vec) return (e < n) ? *reinterpret_cast<const u32x4*>(row + e) : u32x4{0, 0, 0, 0};
-  unsigned short hh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) hh[j] = (e + j < n) ? __half_as_ushort(row[e + j]) : (unsigned short)0;
-  return u32x4{hh[0] | (uint32_t(hh[1]) << 16), hh[2] | (uint32_t(hh[3]) << 16), hh[4] | (uint32_t(hh[5]) << 16),
-               hh[6] | (uint32_t(hh[7]) << 16)};
-}
-
-// Buffer descriptor over `bytes` bytes at `p`, built from provably wave-uniform
-// values (guide T20: no waterfall loops around the buffer ops).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  void* q = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
-template <int V>
-struct IC {
-  static constexpr int value = V;
-};
-
-// One workgroup = NW waves; each wave owns QB blocks of 32 queries of one (batch,
-// head) slice and sweeps the key tiles its rule allows.  With QB = 2 a wave has
-// two independent softmax streams sharing every K/V fragment read, and runs
-// alone on its SIMD (the whole 512-entry register file), so the matrix work of
-// one tile overlaps the vector work of the same wave instead of relying on a
-// partner wave that reaches the same phase at the same time.
+// One workgroup = NW waves; each wave owns 32 queries of one (batch, head) slice
+// and sweeps the key tiles its rule allows.
 //   POL 0: full policy (only the nk tail tile is masked)
 //       1: interval rules (causal, 1d unit-stride local): per-lane key interval,
 //          tile class from the wave's bounds, skipped tiles cost nothing.
-constexpr int fast_waves_per_eu(int D, int QB, int F) { return (D >= 128 || QB > 1) ? 1 : ((F & kFOcc3) ? 3 : 2); }
-
-template <int D, int NW, int QB, int POL, int F>
-__global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D, QB, F)) void fwd_f16_fast_kernel(FwdArgs a) {
+template <int D, int NW, int POL, int F>
+__global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
-  using S = FastSmem<D, NW * QB>;
+  constexpr int TPB = (F & kFTpb2) ? 2 : 1;
+  using S = FastSmem<D, NW, TPB>;
+  constexpr int NS = S::kNS;
   constexpr int kThr = NW * 64;
   constexpr int kBM = S::kBM;
   constexpr int kChunks = D * 8;  // 16-B chunks per K (or V) tile
@@ -159,20 +104,19 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D, QB, F)) void fwd_f16_
   const int ntiles = (ke > kb) ? (ke - kt0 + kBN - 1) / kBN : 0;
 
   // ---- staging: chunk j of this thread = 8 keys of channel row c
-  uint32_t voff[kCPT];
-  uint32_t kwo[kCPT], vwo[kCPT];
+  uint32_t voff[kCPT], kwo[kCPT], vwo[kCPT];
   const int cm = tid & 7;  // chunk index within the 64-key row (same for every j)
 #pragma unroll
   for (int j = 0; j < kCPT; ++j) {
     const int c = (tid + kThr * j) >> 3;
     voff[j] = (uint32_t)c * (uint32_t)nk * 2u + 16u * cm;
-    kwo[j] = c * 128 + ((cm * 16) ^ ((c & 2) << 5));          // K: 64-B halves swapped on rows with c&2
+    kwo[j] = c * 128 + ((cm * 16) ^ ((c & 2) << 5));  // K: 64-B halves swapped on rows with c&2
     // V: group (s, h) = keys {16s + 4h + 0..3, 16s + 8 + 4h + 0..3}, [v][8 keys] rows, so one
     // ds_read_b128 is a PV A operand; chunk cm = keys 8cm..8cm+7 -> groups (cm/2, 0) and (cm/2, 1)
     vwo[j] = ((2 * (cm >> 1)) * (D + kVPad) + c) * 16 + (cm & 1) * 8;
   }
-  constexpr int NSET = (F & kFDeep) ? 2 : 1;
-  u32x4 kr[NSET][kCPT], vr[NSET][kCPT];
+  // register staging: TPB K tiles and TPB V tiles loaded one barrier phase ahead of their store
+  u32x4 kr[TPB][kCPT], vr[TPB][kCPT];
   auto load_into = [&](u32x4 (&dst)[kCPT], __amdgpu_buffer_rsrc_t rs, int k0) {
     if (k0 + kBN <= nk) {
 #pragma unroll
@@ -180,8 +124,7 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D, QB, F)) void fwd_f16_
     } else {  // nk tail: chunks past nk read as zeros (offset beyond the descriptor's range)
       const bool out = k0 + 8 * cm >= nk;
 #pragma unroll
-      for (int j = 0; j < kCPT; ++j)
-        dst[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, out ? 0x80000000u : voff[j], 2 * k0, 0);
+      for (int j = 0; j < kCPT; ++j) dst[j] = buf_load16(rs, voff[j], 2 * k0, out);
     }
   };
   auto store_k = [&](int slot, const u32x4 (&src)[kCPT]) {
@@ -198,73 +141,70 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D, QB, F)) void fwd_f16_
     }
   };
 
-  // ---- prologue loads: K(0), V(0), K(1) in flight together with the Q tile
-  u32x4 kr1[kCPT];
-  if (ntiles > 0) { load_into(kr[0], krs, kt0); load_into(vr[0], vrs, kt0); }
-  if (ntiles > 1) load_into(kr1, krs, kt0 + kBN);
-  for (int idx = tid; idx < D * (kBM / 8); idx += kThr) {  // Q [D][BM], 64-B blocks XOR-swizzled by c&3
-    const int c = idx / (kBM / 8), m = idx % (kBM / 8);
-    const u32x4 v = load_chunk_q(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec);
-    *reinterpret_cast<lds_u32x4_t*>(smem + c * S::kQRow + ((m * 16) ^ ((c & 3) << 6))) = v;
-  }
-  if (ntiles > 0) { store_k(0, kr[0]); store_v(0, vr[0]); }
-  if (ntiles > 1) store_k(1, kr1);
-  // register set x feeds the stores of iterations with parity x: K(it+2), V(it+1)
+  // ---- prologue: K(0..TPB), V(0..TPB-1) into the ring, K(TPB+1..2TPB) / V(TPB..2TPB-1) into
+  //      the staging registers; all in flight together with the Q tile
+  {
+    u32x4 pk[TPB + 1][kCPT], pv[TPB][kCPT];
 #pragma unroll
-  for (int x = 0; x < NSET; ++x) {
-    if (ntiles > 2 + x) load_into(kr[x], krs, kt0 + (2 + x) * kBN);
-    if (ntiles > 1 + x) load_into(vr[x], vrs, kt0 + (1 + x) * kBN);
+    for (int x = 0; x <= TPB; ++x)
+      if (x < ntiles) load_into(pk[x], krs, kt0 + x * kBN);
+#pragma unroll
+    for (int x = 0; x < TPB; ++x)
+      if (x < ntiles) load_into(pv[x], vrs, kt0 + x * kBN);
+    for (int idx = tid; idx < D * (kBM / 8); idx += kThr) {  // Q [D][BM], 64-B blocks XOR-swizzled by c&3
+      const int c = idx / (kBM / 8), m = idx % (kBM / 8);
+      const u32x4 v = load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec);
+      *reinterpret_cast<lds_u32x4_t*>(smem + c * S::kQRow + ((m * 16) ^ ((c & 3) << 6))) = v;
+    }
+#pragma unroll
+    for (int x = 0; x <= TPB; ++x)
+      if (x < ntiles) store_k(x, pk[x]);
+#pragma unroll
+    for (int x = 0; x < TPB; ++x)
+      if (x < ntiles) store_v(x, pv[x]);
+#pragma unroll
+    for (int x = 0; x < TPB; ++x) {
+      if (TPB + 1 + x < ntiles) load_into(kr[x], krs, kt0 + (TPB + 1 + x) * kBN);
+      if (TPB + x < ntiles) load_into(vr[x], vrs, kt0 + (TPB + x) * kBN);
+    }
   }
   __syncthreads();
 
-  // Q*scale*log2(e) as the B operand of Sᵀ = Kᵀ·Q: lane (r,h) of block j holds
-  // Q[c = 16s + 8h + e][q = 32(QB*w + j) + r]
-  half8 qf[QB][D / 16];
+  // Q*scale*log2(e) as the B operand of Sᵀ = Kᵀ·Q: lane (r,h) holds Q[c = 16s + 8h + e][q = 32w + r]
+  half8 qf[D / 16];
 #pragma unroll
-  for (int j = 0; j < QB; ++j)
+  for (int s = 0; s < D / 16; ++s) {
 #pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int crow = 16 * s + 8 * (g >> 1) + 4 * e + tq;
-        const int col = 32 * (QB * w + j) + 16 * (g & 1) + 4 * tp;
-        const half4 t = tr_read(smem + crow * S::kQRow + ((col * 2) ^ ((crow & 3) << 6)));
-        if (e == 0) qf[j][s].lo = t; else qf[j][s].hi = t;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) qf[j][s][e] = (_Float16)((float)qf[j][s][e] * c2);
+    for (int e = 0; e < 2; ++e) {
+      const int crow = 16 * s + 8 * (g >> 1) + 4 * e + tq;
+      const int col = 32 * w + 16 * (g & 1) + 4 * tp;
+      const half4 t = tr_read(smem + crow * S::kQRow + ((col * 2) ^ ((crow & 3) << 6)));
+      if (e == 0) qf[s].lo = t; else qf[s].hi = t;
     }
+    qf[s] = scale8(qf[s], c2);
+  }
 
-  const int wq0 = q0 + 32 * QB * w;
+  const int wq0 = q0 + 32 * w;
+  const int qi = wq0 + r;
   const bool wave_active = wq0 < nq;
-  // POL 1: each lane's allowed keys [klo, klo + kspan) per block, and the wave's bounds on them
+  // POL 1: this lane's allowed keys [klo, klo + kspan) and the wave's bounds on them
   // (both interval ends are non-decreasing in the query, so the first / last valid lane bound them)
-  int klo[QB], kspan[QB];
-  int wlo_min = 0, wlo_max = 0, whi_min = 0, whi_max = 0;
-#pragma unroll
-  for (int j = 0; j < QB; ++j) { klo[j] = 0; kspan[j] = 0; }
+  int klo = 0, kspan = 0, wlo_min = 0, wlo_max = 0, whi_min = 0, whi_max = 0;
   if (POL == 1 && wave_active) {
-    int khi[QB];
-#pragma unroll
-    for (int j = 0; j < QB; ++j) {
-      key_interval(a.rule, min(wq0 + 32 * j + r, nq - 1), &klo[j], &khi[j]);
-      kspan[j] = max(khi[j] - klo[j] + 1, 0);
-    }
-    const int last = min(32 * QB - 1, nq - 1 - wq0);  // last valid query of the wave
-    wlo_min = __builtin_amdgcn_readfirstlane(klo[0]);
-    whi_min = __builtin_amdgcn_readfirstlane(khi[0]);
-    int lo_last = klo[0], hi_last = khi[0];
-#pragma unroll
-    for (int j = 1; j < QB; ++j)
-      if (last >= 32 * j) { lo_last = klo[j]; hi_last = khi[j]; }
-    wlo_max = __builtin_amdgcn_readlane(lo_last, last & 31);
-    whi_max = __builtin_amdgcn_readlane(hi_last, last & 31);
+    int khi;
+    key_interval(a.rule, min(qi, nq - 1), &klo, &khi);
+    kspan = max(khi - klo + 1, 0);
+    const int last = min(31, nq - 1 - wq0);
+    wlo_min = __builtin_amdgcn_readfirstlane(klo);
+    whi_min = __builtin_amdgcn_readfirstlane(khi);
+    wlo_max = __builtin_amdgcn_readlane(klo, last);
+    whi_max = __builtin_amdgcn_readlane(khi, last);
   }
   // tile class for this wave: 0 no allowed pair (skipped), 1 mixed (per-element mask), 2 all
   auto tcls = [&](int k0) -> int {
     const int k1 = k0 + kBN - 1;
     if (!wave_active) return 0;
-    if (POL == 0) return (k1 < nk && wq0 + 32 * QB <= nq) ? 2 : 1;
+    if (POL == 0) return (k1 < nk && wq0 + 32 <= nq) ? 2 : 1;
     if (wlo_min > k1 || whi_max < k0) return 0;
     return (wlo_max <= k0 && whi_min >= k1 && k1 < nk) ? 2 : 1;
   };
@@ -276,28 +216,22 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D, QB, F)) void fwd_f16_
   //   V: lane (r,h) reads group (s, h), channel row 32u + r
   const uint32_t vbase = (h * (D + kVPad) + r) * 16;
 
-  floatx16 acc_o[QB][D / 32];
+  floatx16 acc_o[D / 32];
 #pragma unroll
-  for (int j = 0; j < QB; ++j)
+  for (int u = 0; u < D / 32; ++u)
 #pragma unroll
-    for (int u = 0; u < D / 32; ++u)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc_o[j][u][i] = 0.f;
+    for (int i = 0; i < 16; ++i) acc_o[u][i] = 0.f;
   // m_run: lazily moved softmax reference (log2 units) that l_run / acc_o are relative to;
   // negm = -m_run broadcast (the C operand of every Sᵀ chain); m_max: exact row max.
   // thr: rescale trigger — -FLT_MAX until the lane's first allowed key seeds m_run, then
   // kRescaleThr, so the per-tile test is one compare.
   // pend: a rebase of tile it moved m_run after the Sᵀ MFMAs of tile it+1 were issued against
-  // the old value; tile it+1 subtracts it when it becomes current (rare, keeps the in-flight
+  // the old value; tile it+1 subtracts it when it becomes current (rare; keeps the in-flight
   // accumulators out of the rebase branch)
-  float m_run[QB], l_run[QB], l_run2[QB], m_max[QB], thr[QB], pend[QB];
-  floatx16 negm[QB];
+  float m_run = 0.f, l_run = 0.f, l_run2 = 0.f, m_max = kNegInf, thr = -__FLT_MAX__, pend = 0.f;
+  floatx16 negm;
 #pragma unroll
-  for (int j = 0; j < QB; ++j) {
-    m_run[j] = 0.f; l_run[j] = 0.f; l_run2[j] = 0.f; m_max[j] = kNegInf; thr[j] = -__FLT_MAX__; pend[j] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) negm[j][i] = 0.f;
-  }
+  for (int i = 0; i < 16; ++i) negm[i] = 0.f;
 
   auto read_k = [&](int slot, half8 (&kf)[2][D / 16]) {
     const lds_char_t* kb_ = smem + S::offK + slot * S::kK;
@@ -314,248 +248,207 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D, QB, F)) void fwd_f16_
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int u = 0; u < D / 32; ++u)
-        vf[s][u] = *reinterpret_cast<const __attribute__((address_space(3))) half8*>(
-            vb_ + ((2 * s) * (D + kVPad) + 32 * u) * 16);
+      for (int u = 0; u < D / 32; ++u) vf[s][u] = read_b128(vb_ + ((2 * s) * (D + kVPad) + 32 * u) * 16);
   };
-  auto qk = [&](const half8 (&kf)[2][D / 16], floatx16 (&st)[QB][2]) {
+  auto qk = [&](const half8 (&kf)[2][D / 16], floatx16 (&st)[2]) {
 #pragma unroll
     for (int s = 0; s < D / 16; ++s)
 #pragma unroll
-      for (int j = 0; j < QB; ++j)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          st[j][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], qf[j][s], s == 0 ? negm[j] : st[j][t], 0, 0, 0);
+      for (int t = 0; t < 2; ++t)
+        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], qf[s], s == 0 ? negm : st[t], 0, 0, 0);
   };
   // per-element rule / tail mask of a mixed tile
-  auto mask = [&](int k0, floatx16 (&st)[QB][2]) {
+  auto mask = [&](int k0, floatx16 (&st)[2]) {
+    const int base = k0 + 4 * h - klo;
+    const bool qok = qi < nq;
 #pragma unroll
-    for (int j = 0; j < QB; ++j) {
-      const int base = k0 + 4 * h - klo[j];
-      const bool qok = wq0 + 32 * j + r < nq;
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int off = 32 * t + (i & 3) + 8 * (i >> 2);
-          const bool ok = (POL == 1) ? ((unsigned)(base + off) < (unsigned)kspan[j]) : (qok && (k0 + off + 4 * h < nk));
-          st[j][t][i] = ok ? st[j][t][i] : kNegInf;
-        }
-    }
-  };
-  // row max of tile `st` (lanes l and l^32 together) -> mt
-  auto rowmax = [&](floatx16 (&st)[QB][2], float (&mt)[QB]) {
-#pragma unroll
-    for (int j = 0; j < QB; ++j) {
-      float mx0 = fmaxf(st[j][0][0], st[j][0][1]), mx1 = fmaxf(st[j][1][0], st[j][1][1]);
-#pragma unroll
-      for (int i = 2; i < 16; i += 2) {
-        mx0 = fmaxf(fmaxf(mx0, st[j][0][i]), st[j][0][i + 1]);
-        mx1 = fmaxf(fmaxf(mx1, st[j][1][i]), st[j][1][i + 1]);
+      for (int i = 0; i < 16; ++i) {
+        const int off = 32 * t + (i & 3) + 8 * (i >> 2);
+        const bool ok = (POL == 1) ? ((unsigned)(base + off) < (unsigned)kspan) : (qok && (k0 + off + 4 * h < nk));
+        st[t][i] = ok ? st[t][i] : kNegInf;
       }
-      mt[j] = (F & kANoMax) ? st[j][0][0] * 0.f : max_pair32(fmaxf(mx0, mx1));
-      m_max[j] = fmaxf(m_max[j], m_run[j] + mt[j]);
+  };
+  // row max of tile `st` (lanes l and l^32 together)
+  auto rowmax = [&](floatx16 (&st)[2]) -> float {
+    float mx0 = fmaxf(st[0][0], st[0][1]), mx1 = fmaxf(st[1][0], st[1][1]);
+#pragma unroll
+    for (int i = 2; i < 16; i += 2) {
+      mx0 = fmaxf(fmaxf(mx0, st[0][i]), st[0][i + 1]);
+      mx1 = fmaxf(fmaxf(mx1, st[1][i]), st[1][i + 1]);
     }
+    const float mt = (F & kANoMax) ? st[0][0] * 0.f : max_pair32(fmaxf(mx0, mx1));
+    m_max = fmaxf(m_max, m_run + mt);
+    return mt;
   };
   // lazy rebase (rare): after it exp2(st) are the tile's probabilities relative to m_run
-  auto rebase = [&](const float (&mt)[QB], floatx16 (&st)[QB][2], bool has_next) {
-    bool fire = false;
+  auto rebase = [&](float mt, floatx16 (&st)[2], bool has_next) {
+    if (__any(mt > thr)) {  // rare: seed, or the tile max moved past the threshold
+      const bool unset = thr < 0.f;
+      const bool seed = unset && (mt > thr);
+      const float delta = unset ? (seed ? mt : 0.f) : fmaxf(mt, 0.f);
+      const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
+      m_run += delta;
+      thr = (unset && !seed) ? thr : kRescaleThr;
+      l_run *= alpha;
+      l_run2 *= alpha;
 #pragma unroll
-    for (int j = 0; j < QB; ++j) fire |= mt[j] > thr[j];
-    if (__any(fire)) {  // rare: seed, or a tile max moved past the threshold
+      for (int u = 0; u < D / 32; ++u)
 #pragma unroll
-      for (int j = 0; j < QB; ++j) {
-        const bool unset = thr[j] < 0.f;
-        const bool seed = unset && (mt[j] > thr[j]);
-        const float delta = unset ? (seed ? mt[j] : 0.f) : fmaxf(mt[j], 0.f);
-        const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
-        m_run[j] += delta;
-        thr[j] = (unset && !seed) ? thr[j] : kRescaleThr;
-        l_run[j] *= alpha;
-        l_run2[j] *= alpha;
+        for (int i = 0; i < 16; ++i) acc_o[u][i] *= alpha;
 #pragma unroll
-        for (int u = 0; u < D / 32; ++u)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) acc_o[j][u][i] *= alpha;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          st[j][0][i] -= delta;
-          st[j][1][i] -= delta;
-          negm[j][i] = -m_run[j];
-        }
-        pend[j] = has_next ? delta : 0.f;  // the next tile's in-flight scores used the old m_run
+      for (int i = 0; i < 16; ++i) {
+        st[0][i] -= delta;
+        st[1][i] -= delta;
+        negm[i] = -m_run;
       }
+      pend = has_next ? delta : 0.f;  // the next tile's in-flight scores used the old m_run
     }
   };
   // P = exp2(st) (fp16) as the B operand of Oᵀ = V·Pᵀ; row sums; PV MFMAs
-  auto exp_pv = [&](floatx16 (&st)[QB][2], const half8 (&vf)[4][D / 32]) {
+  auto exp_pv = [&](floatx16 (&st)[2], const half8 (&vf)[4][D / 32]) {
     const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < 4; ++s) {
+      half8 pf;
+      if (F & kFSumAdd) {
+        float e[8];
 #pragma unroll
-      for (int j = 0; j < QB; ++j) {
-        half8 pf;
-        if (F & kFSumAdd) {
-          float e[8];
+        for (int x = 0; x < 8; ++x) e[x] = __builtin_amdgcn_exp2f(st[s >> 1][8 * (s & 1) + x]);
 #pragma unroll
-          for (int x = 0; x < 8; ++x) e[x] = __builtin_amdgcn_exp2f(st[j][s >> 1][8 * (s & 1) + x]);
-#pragma unroll
-          for (int x = 0; x < 8; x += 2) {
-            l_run[j] += e[x];
-            l_run2[j] += e[x + 1];
-          }
-#pragma unroll
-          for (int x = 0; x < 8; ++x) pf[x] = (_Float16)e[x];
-        } else {
-#pragma unroll
-          for (int x = 0; x < 8; ++x) {
-            const float sv = st[j][s >> 1][8 * (s & 1) + x];
-            pf[x] = (_Float16)((F & kANoExp) ? sv : __builtin_amdgcn_exp2f(sv));
-          }
-#pragma unroll
-          for (int x = 0; x < 8; x += 4) {
-            l_run[j] = __builtin_amdgcn_fdot2(half2v{pf[x], pf[x + 1]}, one2, l_run[j], false);
-            l_run2[j] = __builtin_amdgcn_fdot2(half2v{pf[x + 2], pf[x + 3]}, one2, l_run2[j], false);
-          }
+        for (int x = 0; x < 8; x += 2) {
+          l_run += e[x];
+          l_run2 += e[x + 1];
         }
 #pragma unroll
-        for (int u = 0; u < D / 32; ++u) {
-          if (F & kANoPV) acc_o[j][u][0] += (float)pf[u] + (float)vf[s][u][0];
-          else acc_o[j][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], pf, acc_o[j][u], 0, 0, 0);
+        for (int x = 0; x < 8; ++x) pf[x] = (_Float16)e[x];
+      } else {
+#pragma unroll
+        for (int x = 0; x < 8; ++x) {
+          const float sv = st[s >> 1][8 * (s & 1) + x];
+          pf[x] = (_Float16)((F & kANoExp) ? sv : __builtin_amdgcn_exp2f(sv));
+        }
+#pragma unroll
+        for (int x = 0; x < 8; x += 4) {
+          l_run = __builtin_amdgcn_fdot2(half2v{pf[x], pf[x + 1]}, one2, l_run, false);
+          l_run2 = __builtin_amdgcn_fdot2(half2v{pf[x + 2], pf[x + 3]}, one2, l_run2, false);
         }
       }
+#pragma unroll
+      for (int u = 0; u < D / 32; ++u) {
+        if (F & kANoPV) acc_o[u][0] += (float)pf[u] + (float)vf[s][u][0];
+        else acc_o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], pf, acc_o[u], 0, 0, 0);
+      }
+    }
   };
 
   // ---- S(0)
-  floatx16 stA[QB][2], stB[QB][2];
+  floatx16 stA[2], stB[2];
   if (ntiles > 0 && tcls(kt0) != 0) {
     half8 kf[2][D / 16];
     read_k(0, kf);
     qk(kf, stA);
   }
 
-  // iteration it: K(it+1) in slot (it+1)&1, V(it) in slot it&1 (both complete after the barrier);
-  // K(it+2) -> slot it&1 and V(it+1) -> slot (it+1)&1 (both finished with in iteration it-1).
-  // Order: [mask(it) if mixed] [Sᵀ MFMAs of it+1 beside the row max of it] [rare rebase]
-  //        [exp2 / convert / row sums of it beside its PV MFMAs]
-  uint64_t dsum[7] = {0, 0, 0, 0, 0, 0, 0};
-  uint64_t tprev = 0;
-  auto stamp = [&]() -> uint64_t {
-    uint64_t t = 0;
-    if (F & kDiag) {
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-      __builtin_amdgcn_sched_barrier(0);
+  // tile it (c = it mod NS, static after the unroll): K(it+1) in slot (c+1)%NS, V(it) in slot c.
+  // A barrier phase starts at every tile with c % TPB == 0 (phase tiles it..it+TPB-1) and
+  //   stores K(it+TPB+1 .. it+2TPB) into slots (c+TPB+1 .. c+2TPB)%NS  (read in the previous phase),
+  //   stores V(it+TPB .. it+2TPB-1) into slots (c+TPB .. c+2TPB-1)%NS   (read in the previous phase),
+  //   loads K(it+2TPB+1 ..) and V(it+2TPB ..) into the staging registers (stored next phase).
+  // Order within a tile: [mask(it) if mixed] [Sᵀ MFMAs of it+1 beside the row max of it]
+  //                      [rare rebase] [V reads] [exp2 / convert / row sums of it beside its PV MFMAs]
+  auto step = [&](auto C_, int it, floatx16 (&cur)[2], floatx16 (&nxt)[2]) {
+    constexpr int c = decltype(C_)::value;
+    if (c % TPB == 0) {
+      if (!(F & kANoBar)) __syncthreads();
+#pragma unroll
+      for (int x = 0; x < TPB; ++x) {
+        if (it + TPB + 1 + x < ntiles) store_k((c + TPB + 1 + x) % NS, kr[x]);
+        if (it + TPB + x < ntiles) store_v((c + TPB + x) % NS, vr[x]);
+      }
+      if (!(F & kANoLoad)) {
+#pragma unroll
+        for (int x = 0; x < TPB; ++x) {
+          if (it + 2 * TPB + 1 + x < ntiles) load_into(kr[x], krs, kt0 + (it + 2 * TPB + 1 + x) * kBN);
+          if (it + 2 * TPB + x < ntiles) load_into(vr[x], vrs, kt0 + (it + 2 * TPB + x) * kBN);
+        }
+      }
     }
-    return t;
-  };
-  auto step = [&](auto P_, int it, floatx16 (&cur)[QB][2], floatx16 (&nxt)[QB][2]) {
-    constexpr int p = decltype(P_)::value;  // it & 1
-    const uint64_t t0 = stamp();
-    if (!(F & kANoBar)) __syncthreads();
-    const uint64_t t1 = stamp();
     const int k0 = kt0 + it * kBN;
     const int ccur = tcls(k0);
     const bool has_next = it + 1 < ntiles;
     const int cnxt = has_next ? tcls(k0 + kBN) : 0;
     half8 kf[2][D / 16];
     half8 vf[4][D / 32];
-    if (cnxt != 0) read_k(p ^ 1, kf);
-    if (ccur != 0 && !(F & kFLateV)) read_v(p, vf);
-    const uint64_t ta = stamp();
-    constexpr int rs = (NSET == 2) ? p : 0;
-    if (it + 2 < ntiles) store_k(p, kr[rs]);
-    if (has_next) store_v(p ^ 1, vr[rs]);
-    const uint64_t tb = stamp();
-    if (!(F & kANoLoad)) {
-      if (it + 2 + NSET < ntiles) load_into(kr[rs], krs, k0 + (2 + NSET) * kBN);
-      if (it + 1 + NSET < ntiles) load_into(vr[rs], vrs, k0 + (1 + NSET) * kBN);
-    }
-    bool adj = false;
+    if (cnxt != 0) read_k((c + 1) % NS, kf);
+    if (ccur != 0 && !(F & kFLateV)) read_v(c, vf);
+    if (__any(pend != 0.f)) {  // rare: this tile's scores predate the last rebase
 #pragma unroll
-    for (int j = 0; j < QB; ++j) adj |= pend[j] != 0.f;
-    if (__any(adj)) {  // rare: this tile's scores predate the last rebase
-#pragma unroll
-      for (int j = 0; j < QB; ++j) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          cur[j][0][i] -= pend[j];
-          cur[j][1][i] -= pend[j];
-        }
-        pend[j] = 0.f;
+      for (int i = 0; i < 16; ++i) {
+        cur[0][i] -= pend;
+        cur[1][i] -= pend;
       }
+      pend = 0.f;
     }
     if (ccur == 1) mask(k0, cur);
-    const uint64_t t2 = stamp();
-    float mt[QB];
+    float mt = 0.f;
     if (cnxt != 0 && ccur != 0) {  // one basic block: next tile's MFMAs beside this tile's max
       if (!(F & kANoQK)) qk(kf, nxt);
-      rowmax(cur, mt);
+      mt = rowmax(cur);
     } else {
       if (cnxt != 0 && !(F & kANoQK)) qk(kf, nxt);
-      if (ccur != 0) rowmax(cur, mt);
+      if (ccur != 0) mt = rowmax(cur);
     }
-    const uint64_t t3 = stamp();
     if (ccur != 0) {
       rebase(mt, cur, cnxt != 0);
-      if (F & kFLateV) read_v(p, vf);
+      if (F & kFLateV) read_v(c, vf);
       exp_pv(cur, vf);
     }
-    const uint64_t t4 = stamp();
-    if (F & kDiag) {
-      dsum[0] += t1 - t0; dsum[1] += t2 - tb; dsum[5] += ta - t1; dsum[6] += tb - ta; dsum[2] += t3 - t2; dsum[3] += t4 - t3;
-      if (tprev) dsum[4] += t0 - tprev;
-      tprev = t4;
-    }
   };
-  for (int it = 0; it < ntiles; it += 2) {
+  for (int it = 0; it < ntiles; it += NS) {
     step(IC<0>{}, it, stA, stB);
     if (it + 1 < ntiles) step(IC<1>{}, it + 1, stB, stA);
+    if (NS > 2) {
+      if (it + 2 < ntiles) step(IC<2 % NS>{}, it + 2, stA, stB);
+      if (it + 3 < ntiles) step(IC<3 % NS>{}, it + 3, stB, stA);
+    }
   }
 
-  if (F & kDiag) {  // barrier, reads+stores+loads+mask, QK+max, rebase+exp+PV, loop overhead
-    if (lane == 0 && wave_active)
-      for (int x = 0; x < 7; ++x) static_cast<float*>(a.l)[bi * (int64_t)nq + wq0 + x] = (float)dsum[x];
-    return;
-  }
   if (!wave_active) return;
+  const float l_tot = sum_pair32(l_run + l_run2);
+  const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
+  if (qi < nq) {
+    __half* O = static_cast<__half*>(a.O) + bi * (int64_t)D * nq;
 #pragma unroll
-  for (int j = 0; j < QB; ++j) {
-    const int qi = wq0 + 32 * j + r;
-    const float l_tot = sum_pair32(l_run[j] + l_run2[j]);
-    const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
-    if (qi < nq) {
-      __half* O = static_cast<__half*>(a.O) + bi * (int64_t)D * nq;
+    for (int u = 0; u < D / 32; ++u)
 #pragma unroll
-      for (int u = 0; u < D / 32; ++u)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int v = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-          O[(int64_t)v * nq + qi] = __float2half(acc_o[j][u][i] * inv);
-        }
-      if (h == 0) {
-        float* lo = static_cast<float*>(a.l) + bi * (int64_t)nq;
-        __half* mo = static_cast<__half*>(a.m) + bi * (int64_t)nq;
-        if (l_tot > 0.f) {
-          const __half mT = __float2half(m_max[j] * kLn2);
-          // l relative to the STORED (rounded) m, so exp(s - m)/l is exact downstream
-          lo[qi] = l_tot * __builtin_amdgcn_exp2f(m_run[j] - __half2float(mT) * kLog2e);
-          mo[qi] = mT;
-        } else {
-          lo[qi] = 0.f;
-          mo[qi] = neg_inf_approx<__half>();
-        }
+      for (int i = 0; i < 16; ++i) {
+        const int v = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+        O[(int64_t)v * nq + qi] = __float2half(acc_o[u][i] * inv);
+      }
+    if (h == 0) {
+      float* lo = static_cast<float*>(a.l) + bi * (int64_t)nq;
+      __half* mo = static_cast<__half*>(a.m) + bi * (int64_t)nq;
+      if (l_tot > 0.f) {
+        const __half mT = __float2half(m_max * kLn2);
+        // l relative to the STORED (rounded) m, so exp(s - m)/l is exact downstream
+        lo[qi] = l_tot * __builtin_amdgcn_exp2f(m_run - __half2float(mT) * kLog2e);
+        mo[qi] = mT;
+      } else {
+        lo[qi] = 0.f;
+        mo[qi] = neg_inf_approx<__half>();
       }
     }
   }
 }
 
-template <int D, int NW, int QB, int F>
+template <int D, int NW, int F>
 hipError_t launch_fast_t(const FwdArgs& a, hipStream_t s) {
-  using S = FastSmem<D, NW * QB>;
+  using S = FastSmem<D, NW, (F & kFTpb2) ? 2 : 1>;
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
   const int smem = S::kTotal;
-  auto kern = a.rule.policy == 0 ? fwd_f16_fast_kernel<D, NW, QB, 0, F> : fwd_f16_fast_kernel<D, NW, QB, 1, F>;
+  auto kern = a.rule.policy == 0 ? fwd_f16_fast_kernel<D, NW, 0, F> : fwd_f16_fast_kernel<D, NW, 1, F>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      smem);
   if (e != hipSuccess) return e;
@@ -579,62 +472,46 @@ bool fwd_f16_fast_supported(const FwdArgs& a) {
 }
 
 hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
-  // FA_FWD_VARIANT = 1<NW><QB><F>: e.g. 1420 = 4 waves x 2 query blocks, flags 0
+  // FA_FWD_VARIANT = 1<NW><F>: e.g. 186 = 8 waves, flags 6 (timing runs); unset -> tuned default
   const int v = fast_variant();
   if (a.d == 64 && v == 1899) {  // ablations (timing only)
     const char* e = getenv("FA_FWD_ABL");
     switch (e ? atoi(e) : 0) {
-      case 64: return launch_fast_t<64, 4, 2, 4 | 64>(a, s);
-      case 128: return launch_fast_t<64, 4, 2, 4 | 128>(a, s);
-      case 256: return launch_fast_t<64, 4, 2, 4 | 256>(a, s);
-      case 512: return launch_fast_t<64, 4, 2, 4 | 512>(a, s);
-      case 1024: return launch_fast_t<64, 4, 2, 4 | 1024>(a, s);
-      case 2048: return launch_fast_t<64, 4, 2, 4 | 2048>(a, s);
-      case 640: return launch_fast_t<64, 4, 2, 4 | 128 | 512>(a, s);
-      case 3072: return launch_fast_t<64, 4, 2, 4 | 1024 | 2048>(a, s);
-      case 4096: return launch_fast_t<64, 8, 1, 2 | 4096>(a, s);
-      case 4100: return launch_fast_t<64, 8, 1, 6 | 4096>(a, s);
-      case 4116: return launch_fast_t<64, 8, 1, 22 | 4096>(a, s);
-      default: return launch_fast_t<64, 4, 2, 4>(a, s);
+      case 64: return launch_fast_t<64, 8, 6 | 64>(a, s);
+      case 128: return launch_fast_t<64, 8, 6 | 128>(a, s);
+      case 256: return launch_fast_t<64, 8, 6 | 256>(a, s);
+      case 512: return launch_fast_t<64, 8, 6 | 512>(a, s);
+      case 1024: return launch_fast_t<64, 8, 6 | 1024>(a, s);
+      case 2048: return launch_fast_t<64, 8, 6 | 2048>(a, s);
+      case 640: return launch_fast_t<64, 8, 6 | 128 | 512>(a, s);
+      case 3072: return launch_fast_t<64, 8, 6 | 1024 | 2048>(a, s);
+      default: return launch_fast_t<64, 8, 6>(a, s);
     }
   }
   if (a.d == 64) {
     switch (v) {
-      case 1810: return launch_fast_t<64, 8, 1, 0>(a, s);
-      case 1812: return launch_fast_t<64, 8, 1, 2>(a, s);
-      case 1410: return launch_fast_t<64, 4, 1, 0>(a, s);
-      case 1418: return launch_fast_t<64, 4, 1, 8>(a, s);
-      case 1412: return launch_fast_t<64, 4, 1, 2>(a, s);
-      case 1414: return launch_fast_t<64, 4, 1, 4>(a, s);
-      case 1416: return launch_fast_t<64, 4, 1, 6>(a, s);
-      case 1814: return launch_fast_t<64, 8, 1, 4>(a, s);
-      case 1830: return launch_fast_t<64, 8, 1, 20>(a, s);
-      case 1832: return launch_fast_t<64, 8, 1, 22>(a, s);
-      case 1430: return launch_fast_t<64, 4, 1, 20>(a, s);
-      case 1816: return launch_fast_t<64, 8, 1, 6>(a, s);
-      case 1419: return launch_fast_t<64, 4, 1, 12>(a, s);
-      case 14110: return launch_fast_t<64, 4, 1, 10>(a, s);
-      case 1420: return launch_fast_t<64, 4, 2, 0>(a, s);
-      case 1421: return launch_fast_t<64, 4, 2, 1>(a, s);
-      case 1220: return launch_fast_t<64, 2, 2, 0>(a, s);
-      case 1820: return launch_fast_t<64, 8, 2, 4>(a, s);
-      case 1425: return launch_fast_t<64, 4, 2, 5>(a, s);
-      case 1426: return launch_fast_t<64, 4, 2, 6>(a, s);
-      case 1424: return launch_fast_t<64, 4, 2, 4>(a, s);
-      // tuned (c2, MI355X): 8 waves x 32 queries, static priority for waves 4-7, late V reads
-      default: return launch_fast_t<64, 8, 1, kFPrio | kFLateV>(a, s);
+      case 180: return launch_fast_t<64, 8, 0>(a, s);
+      case 182: return launch_fast_t<64, 8, 2>(a, s);
+      case 186: return launch_fast_t<64, 8, 6>(a, s);
+      case 188: return launch_fast_t<64, 8, 8>(a, s);
+      case 1814: return launch_fast_t<64, 8, 14>(a, s);
+      case 146: return launch_fast_t<64, 4, 6>(a, s);
+      case 144: return launch_fast_t<64, 4, 4>(a, s);
+      case 1414: return launch_fast_t<64, 4, 14>(a, s);
+      case 1412: return launch_fast_t<64, 4, 12>(a, s);
+      default:
+        // tuned on MI355X: full-length key loops (c2) 8 waves x 32 queries, two key tiles per
+        // barrier; rule-bounded short loops (local windows, c4) 4-wave blocks with one tile per
+        // barrier (48 KB of LDS) so two blocks per CU cover each other's prologue / epilogue
+        if (a.rule.policy == 2) return launch_fast_t<64, 4, kFPrio | kFLateV>(a, s);
+        return launch_fast_t<64, 8, kFPrio | kFLateV | kFTpb2>(a, s);
     }
   }
   switch (v) {
-    case 1411: return launch_fast_t<128, 4, 1, 1>(a, s);
-    case 1412: return launch_fast_t<128, 4, 1, 2>(a, s);
-    case 1414: return launch_fast_t<128, 4, 1, 4>(a, s);
-    case 1416: return launch_fast_t<128, 4, 1, 6>(a, s);
-    case 1810: return launch_fast_t<128, 8, 1, 0>(a, s);
-    case 1814: return launch_fast_t<128, 8, 1, 4>(a, s);
-    case 1410: return launch_fast_t<128, 4, 1, 0>(a, s);
+    case 140: return launch_fast_t<128, 4, 0>(a, s);
+    case 146: return launch_fast_t<128, 4, 6>(a, s);
     // tuned (c3 forward, MI355X): 4 waves (one per SIMD), static priority, late V reads
-    default: return launch_fast_t<128, 4, 1, kFPrio | kFLateV>(a, s);
+    default: return launch_fast_t<128, 4, kFPrio | kFLateV>(a, s);
   }
 }
 
