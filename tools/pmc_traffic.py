@@ -21,13 +21,17 @@ sys.path.insert(0, ROOT)
 
 
 def counter_means(root, regex):
+    """Per counter: the sum over matching kernels of each kernel's mean per dispatch (a step that
+    launches several kernels, e.g. forward + backward, is priced as one step), and the dispatches."""
     vals = {}
     for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True)):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if regex.search(row.get("Kernel_Name", "")):
-                    vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-    return {k: (sum(v) / len(v), len(v)) for k, v in vals.items()}
+                name = row.get("Kernel_Name", "")
+                if regex.search(name):
+                    vals.setdefault(row["Counter_Name"], {}).setdefault(name, []).append(float(row["Counter_Value"]))
+    return {c: (sum(sum(v) / len(v) for v in per.values()), sum(len(v) for v in per.values()))
+            for c, per in vals.items()}
 
 
 def algorithmic_bytes(cfg_key):
