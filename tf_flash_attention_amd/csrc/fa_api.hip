@@ -216,6 +216,8 @@ int fa_backward(void* stream, const fa_problem* p, const void* Q, const void* K,
     if (e == hipSuccess && a.rule.k.n) e = hipMemsetAsync(dV, 0, es * (size_t)a.b * a.v_d * a.rule.k.n, s);
   } else if (p->dtype == FA_F16 && fa::bwd_f16_supported(a)) {
     e = fa::launch_bwd_f16(a, s);
+  } else if (p->dtype == FA_F32 && fa::bwd_f32_supported(a)) {
+    e = fa::launch_bwd_f32(a, s);
   } else {
     if (p->d > fa::generic_max_channels(p->dtype) || p->v_d > fa::generic_max_channels(p->dtype))
       return set_error(FA_ERR_UNSUPPORTED, "channel dimension exceeds the supported maximum for this dtype");
@@ -292,7 +294,7 @@ const char* fa_error_string(int status) {
 const char* fa_last_error(void) { return g_last_error.c_str(); }
 
 const char* fa_build_info(void) {
-  return "tf_flash_attention_amd: gfx950; fwd={mfma_f16, mfma_f32, generic(f16,f32,f64)}; bwd={generic(f16,f32,f64), mfma_f16}";
+  return "tf_flash_attention_amd: gfx950; fwd={mfma_f16, mfma_f32, generic(f16,f32,f64)}; bwd={mfma_f16 (two-pass / single-pass), mfma_f32 (two-pass), generic(f16,f32,f64)}";
 }
 
 }  // extern "C"
