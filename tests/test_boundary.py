@@ -193,6 +193,32 @@ def test_op_surface_mirrors_reference_registrations():
         fa.gradient_op_for("Bogus")
 
 
+def _snake(name):
+    return re.sub(r"(?<=[a-z0-9])(?=[A-Z])", "_", name).lower()
+
+
+def test_tf_op_library_registers_the_same_ops():
+    """tf_op/fa_tf_ops.cc (the TensorFlow-ROCm op library; not buildable here) registers exactly
+    the 30 op names the Python mirror exposes — expanded from its registration macros."""
+    src = open(os.path.join(os.path.dirname(__file__), "..", "tf_flash_attention_amd", "tf_op",
+                            "fa_tf_ops.cc")).read()
+    dims = [int(x) for x in re.findall(r"^FA_REGISTER_OPS\((\d)\)", src, re.M)]
+    body = src[src.index("#define FA_REGISTER_OPS(sd)"):].split("\n\n")[0]
+    ops, kernels = set(), set()
+    for sd in dims:
+        for kind, fam in re.findall(r"FA_REGISTER_(FORWARD|BACKWARD|FLOPS)_OP\(\"(\w+)\"", body):
+            if kind == "FLOPS":
+                ops.add(f"Estimate{fam}{sd}dFlops")
+            else:
+                ops.update({f"{fam}{sd}dFloat16", f"{fam}{sd}d"})
+    for fam, sd in re.findall(r"^FA_REGISTER_KERNELS\(\"(\w+)\", FA_\w+, (\d)\)", src, re.M):
+        for d in ("Forward", "Backward"):
+            kernels.update({f"{fam}{d}{sd}dFloat16", f"{fam}{d}{sd}d"})
+        kernels.add(f"Estimate{fam}Forward{sd}dFlops")
+    assert len(ops) == 30 and ops == kernels
+    assert {_snake(o) for o in ops} == set(vars(fa._fa_kernel))
+
+
 def test_cpu_tensors_fail_loudly():
     """No CPU fallback: host tensors are rejected, never computed by a slow path."""
     import torch
