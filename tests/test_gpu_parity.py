@@ -214,6 +214,13 @@ def test_f16_fast_paths(d, policy, ws, causal, seq_dims, mode, qs, ks):
     run_case(np.float16, policy, seq_dims, mode, (2, 2), d, d, qs, ks, ws=ws, ls=0, causal=causal, seed=d + ws)
 
 
+# channel counts below the kernel's D (zero-padded rows) and d != v_d on the streamlined paths
+@pytest.mark.parametrize("d,vd", [(96, 96), (40, 64), (64, 48), (128, 72), (33, 100)])
+@pytest.mark.parametrize("policy", ["full", "causal"])
+def test_f16_fast_paths_padded_channels(d, vd, policy):
+    run_case(np.float16, policy, 1, "none_front", (2,), d, vd, (200,), (136,), seed=d + vd)
+
+
 @pytest.mark.parametrize("d", [16, 32, 48, 64, 96, 128])
 @pytest.mark.parametrize("policy", ["full", "causal", "local"])
 @pytest.mark.parametrize("nq,nk", [(256, 256), (130, 1001)])

@@ -128,10 +128,12 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const float c2 = (float)a.scale * kLog2e;
 
-  const __half* K = static_cast<const __half*>(a.K) + bi * (int64_t)D * nk;
-  const __half* V = static_cast<const __half*>(a.V) + bi * (int64_t)D * nk;
-  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(static_cast<const __half*>(a.Q) + bi * (int64_t)D * nq, 2u * D * nq);
-  const __amdgpu_buffer_rsrc_t ors = make_rsrc(static_cast<const __half*>(a.dO) + bi * (int64_t)D * nq, 2u * D * nq);
+  // channels d (Q/K) and v_d (V/O) may be smaller than D: rows past them are staged as zeros
+  const int d = a.d, vd = a.v_d;
+  const __half* K = static_cast<const __half*>(a.K) + bi * (int64_t)d * nk;
+  const __half* V = static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk;
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq, 2u * d * nq);
+  const __amdgpu_buffer_rsrc_t ors = make_rsrc(static_cast<const __half*>(a.dO) + bi * (int64_t)vd * nq, 2u * vd * nq);
   const float* glse = static_cast<const float*>(a.ws_lse) + bi * (int64_t)nq;
   const float* gD = static_cast<const float*>(a.ws_D) + bi * (int64_t)nq;
 
@@ -142,7 +144,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       const int which = idx >= D * (kBK / 8);
       const int j = which ? idx - D * (kBK / 8) : idx;
       const int c = j / (kBK / 8), m = j % (kBK / 8);
-      const u32x4 v = load_chunk8((which ? V : K) + (int64_t)c * nk, k0 + 8 * m, nk, true);
+      const u32x4 v = (c < (which ? vd : d)) ? load_chunk8((which ? V : K) + (int64_t)c * nk, k0 + 8 * m, nk, true)
+                                              : u32x4{0, 0, 0, 0};
       *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBK) + ((m * 16) ^ ((c & 3) << 6))) = v;
     }
     __syncthreads();
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) {
       const bool isO = is_o(j);
-      const bool out = qa + 8 * cm_[j] >= nq;
+      const bool out = qa + 8 * cm_[j] >= nq || crow_[j] >= (isO ? vd : d);
       qr[j] = buf_load16(isO ? ors : qrs, voff[j], 2 * qa, out);
     }
     if (tid < 64) {  // lanes 0..31: lse2, 32..63: D
@@ -307,16 +310,16 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 
   // ---- dK = scale·Σ dS·Q, dV: rows c = 32u + (i&3) + 8(i>>2) + 4h, column = this lane's key
   if (!wave_active || key >= nk) return;
-  __half* dK = static_cast<__half*>(a.dK) + bi * (int64_t)D * nk;
-  __half* dV = static_cast<__half*>(a.dV) + bi * (int64_t)D * nk;
+  __half* dK = static_cast<__half*>(a.dK) + bi * (int64_t)d * nk;
+  __half* dV = static_cast<__half*>(a.dV) + bi * (int64_t)vd * nk;
   const float sc = (float)a.scale;
 #pragma unroll
   for (int u = 0; u < D / 32; ++u)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-      dK[(int64_t)c * nk + key] = __float2half(dk[u][i] * sc);
-      dV[(int64_t)c * nk + key] = __float2half(dv[u][i]);
+      if (c < d) dK[(int64_t)c * nk + key] = __float2half(dk[u][i] * sc);
+      if (c < vd) dV[(int64_t)c * nk + key] = __float2half(dv[u][i]);
     }
 }
 
@@ -358,10 +361,11 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const float c2 = (float)a.scale * kLog2e;
 
-  const __half* Q = static_cast<const __half*>(a.Q) + bi * (int64_t)D * nq;
-  const __half* dO = static_cast<const __half*>(a.dO) + bi * (int64_t)D * nq;
-  const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + bi * (int64_t)D * nk, 2u * D * nk);
-  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + bi * (int64_t)D * nk, 2u * D * nk);
+  const int d = a.d, vd = a.v_d;
+  const __half* Q = static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq;
+  const __half* dO = static_cast<const __half*>(a.dO) + bi * (int64_t)vd * nq;
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + bi * (int64_t)d * nk, 2u * d * nk);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk, 2u * vd * nk);
 
   const int wq0 = q0 + 32 * w;
   const int qi = wq0 + r;
@@ -374,7 +378,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
       const int which = idx >= D * (kBM / 8);
       const int j = which ? idx - D * (kBM / 8) : idx;
       const int c = j / (kBM / 8), m = j % (kBM / 8);
-      const u32x4 v = load_chunk8((which ? dO : Q) + (int64_t)c * nq, q0 + 8 * m, nq, true);
+      const u32x4 v = (c < (which ? vd : d)) ? load_chunk8((which ? dO : Q) + (int64_t)c * nq, q0 + 8 * m, nq, true)
+                                              : u32x4{0, 0, 0, 0};
       *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBM) + ((m * 16) ^ ((c & 3) << 6))) = v;
     }
     __syncthreads();
@@ -445,7 +450,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) {
       const bool isV = is_v(j);
-      kr[j] = buf_load16(isV ? vrs : krs, voff[j], 2 * ka, out);
+      kr[j] = buf_load16(isV ? vrs : krs, voff[j], 2 * ka, out || crow_[j] >= (isV ? vd : d));
     }
   };
   auto store_tile = [&](int slot) {
@@ -522,14 +527,14 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   }
 
   if (!wave_active || qi >= nq) return;
-  __half* dQ = static_cast<__half*>(a.dQ) + bi * (int64_t)D * nq;
+  __half* dQ = static_cast<__half*>(a.dQ) + bi * (int64_t)d * nq;
   const float sc = (float)a.scale;
 #pragma unroll
   for (int u = 0; u < D / 32; ++u)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-      dQ[(int64_t)c * nq + qi] = __float2half(dq[u][i] * sc);
+      if (c < d) dQ[(int64_t)c * nq + qi] = __float2half(dq[u][i] * sc);
     }
 }
 
@@ -568,8 +573,9 @@ bool bwd_f16_fast_supported(const BwdArgs& a) {
   const int nq = a.rule.q.n, nk = a.rule.k.n;
   const uintptr_t al = reinterpret_cast<uintptr_t>(a.Q) | reinterpret_cast<uintptr_t>(a.K) |
                        reinterpret_cast<uintptr_t>(a.V) | reinterpret_cast<uintptr_t>(a.dO);
-  return a.d == a.v_d && (a.d == 64 || a.d == 128) && nq > 0 && nk > 0 && nq % 8 == 0 && nk % 8 == 0 &&
-         (al % 16) == 0 && (int64_t)a.d * nq * 2 < (1ll << 31) && (int64_t)a.d * nk * 2 < (1ll << 31) &&
+  const int dm = max(a.d, a.v_d);
+  return dm > 32 && dm <= 128 && nq > 0 && nk > 0 && nq % 8 == 0 && nk % 8 == 0 &&
+         (al % 16) == 0 && (int64_t)dm * nq * 2 < (1ll << 31) && (int64_t)dm * nk * 2 < (1ll << 31) &&
          rule_is_interval(a.rule) && a.b * ((nk + 127) / 128) < (1ll << 31) && a.b * ((nq + 127) / 128) < (1ll << 31);
 }
 
@@ -579,7 +585,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int v = bwd_variant();
-  if (a.d == 64) {
+  if (max(a.d, a.v_d) <= 64) {
     switch (v) {
       case 82: e = launch_dkdv<64, 8, 2>(a, s); break;
       default: e = launch_dkdv<64, 4, 2>(a, s); break;

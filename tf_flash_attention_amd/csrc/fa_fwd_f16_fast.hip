@@ -90,9 +90,11 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_ke
 
   if ((F & kFPrio) && w >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
-  const __half* Q = static_cast<const __half*>(a.Q) + bi * (int64_t)D * nq;
-  const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + bi * (int64_t)D * nk, 2u * D * nk);
-  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + bi * (int64_t)D * nk, 2u * D * nk);
+  // channels d (Q/K) and v_d (V/O) may be smaller than D: rows past them are staged as zeros
+  const int d = a.d, vd = a.v_d;
+  const __half* Q = static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq;
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + bi * (int64_t)d * nk, 2u * d * nk);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk, 2u * vd * nk);
   const bool qvec = ((nq & 7) == 0) && ((reinterpret_cast<uintptr_t>(a.Q) & 15) == 0);
   const float c2 = (float)a.scale * kLog2e;
 
@@ -105,10 +107,12 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_ke
 
   // ---- staging: chunk j of this thread = 8 keys of channel row c
   uint32_t voff[kCPT], kwo[kCPT], vwo[kCPT];
+  int crow[kCPT];
   const int cm = tid & 7;  // chunk index within the 64-key row (same for every j)
 #pragma unroll
   for (int j = 0; j < kCPT; ++j) {
     const int c = (tid + kThr * j) >> 3;
+    crow[j] = c;
     voff[j] = (uint32_t)c * (uint32_t)nk * 2u + 16u * cm;
     kwo[j] = c * 128 + ((cm * 16) ^ ((c & 2) << 5));  // K: 64-B halves swapped on rows with c&2
     // V: group (s, h) = keys {16s + 4h + 0..3, 16s + 8 + 4h + 0..3}, [v][8 keys] rows, so one
@@ -117,14 +121,16 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_ke
   }
   // register staging: TPB K tiles and TPB V tiles loaded one barrier phase ahead of their store
   u32x4 kr[TPB][kCPT], vr[TPB][kCPT];
-  auto load_into = [&](u32x4 (&dst)[kCPT], __amdgpu_buffer_rsrc_t rs, int k0) {
-    if (k0 + kBN <= nk) {
+  // chunks past nk (tail tile) or past the tensor's channel count read as zeros (offset beyond
+  // the descriptor's range)
+  auto load_into = [&](u32x4 (&dst)[kCPT], __amdgpu_buffer_rsrc_t rs, int k0, int rows) {
+    if (k0 + kBN <= nk && rows == D) {
 #pragma unroll
       for (int j = 0; j < kCPT; ++j) dst[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff[j], 2 * k0, 0);
-    } else {  // nk tail: chunks past nk read as zeros (offset beyond the descriptor's range)
+    } else {
       const bool out = k0 + 8 * cm >= nk;
 #pragma unroll
-      for (int j = 0; j < kCPT; ++j) dst[j] = buf_load16(rs, voff[j], 2 * k0, out);
+      for (int j = 0; j < kCPT; ++j) dst[j] = buf_load16(rs, voff[j], 2 * k0, out || crow[j] >= rows);
     }
   };
   auto store_k = [&](int slot, const u32x4 (&src)[kCPT]) {
@@ -147,13 +153,13 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_ke
     u32x4 pk[TPB + 1][kCPT], pv[TPB][kCPT];
 #pragma unroll
     for (int x = 0; x <= TPB; ++x)
-      if (x < ntiles) load_into(pk[x], krs, kt0 + x * kBN);
+      if (x < ntiles) load_into(pk[x], krs, kt0 + x * kBN, d);
 #pragma unroll
     for (int x = 0; x < TPB; ++x)
-      if (x < ntiles) load_into(pv[x], vrs, kt0 + x * kBN);
+      if (x < ntiles) load_into(pv[x], vrs, kt0 + x * kBN, vd);
     for (int idx = tid; idx < D * (kBM / 8); idx += kThr) {  // Q [D][BM], 64-B blocks XOR-swizzled by c&3
       const int c = idx / (kBM / 8), m = idx % (kBM / 8);
-      const u32x4 v = load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec);
+      const u32x4 v = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec) : u32x4{0, 0, 0, 0};
       *reinterpret_cast<lds_u32x4_t*>(smem + c * S::kQRow + ((m * 16) ^ ((c & 3) << 6))) = v;
     }
 #pragma unroll
@@ -164,8 +170,8 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_ke
       if (x < ntiles) store_v(x, pv[x]);
 #pragma unroll
     for (int x = 0; x < TPB; ++x) {
-      if (TPB + 1 + x < ntiles) load_into(kr[x], krs, kt0 + (TPB + 1 + x) * kBN);
-      if (TPB + x < ntiles) load_into(vr[x], vrs, kt0 + (TPB + x) * kBN);
+      if (TPB + 1 + x < ntiles) load_into(kr[x], krs, kt0 + (TPB + 1 + x) * kBN, d);
+      if (TPB + x < ntiles) load_into(vr[x], vrs, kt0 + (TPB + x) * kBN, vd);
     }
   }
   __syncthreads();
@@ -370,8 +376,8 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_ke
       if (!(F & kANoLoad)) {
 #pragma unroll
         for (int x = 0; x < TPB; ++x) {
-          if (it + 2 * TPB + 1 + x < ntiles) load_into(kr[x], krs, kt0 + (it + 2 * TPB + 1 + x) * kBN);
-          if (it + 2 * TPB + x < ntiles) load_into(vr[x], vrs, kt0 + (it + 2 * TPB + x) * kBN);
+          if (it + 2 * TPB + 1 + x < ntiles) load_into(kr[x], krs, kt0 + (it + 2 * TPB + 1 + x) * kBN, d);
+          if (it + 2 * TPB + x < ntiles) load_into(vr[x], vrs, kt0 + (it + 2 * TPB + x) * kBN, vd);
         }
       }
     }
@@ -419,13 +425,13 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_ke
   const float l_tot = sum_pair32(l_run + l_run2);
   const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
   if (qi < nq) {
-    __half* O = static_cast<__half*>(a.O) + bi * (int64_t)D * nq;
+    __half* O = static_cast<__half*>(a.O) + bi * (int64_t)vd * nq;
 #pragma unroll
     for (int u = 0; u < D / 32; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int v = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-        O[(int64_t)v * nq + qi] = __float2half(acc_o[u][i] * inv);
+        if (v < vd) O[(int64_t)v * nq + qi] = __float2half(acc_o[u][i] * inv);
       }
     if (h == 0) {
       float* lo = static_cast<float*>(a.l) + bi * (int64_t)nq;
@@ -465,8 +471,9 @@ int fast_variant() {
 
 bool fwd_f16_fast_supported(const FwdArgs& a) {
   const int nk = a.rule.k.n;
-  return a.d == a.v_d && (a.d == 64 || a.d == 128) && (nk % 8 == 0) && nk > 0 &&
-         (int64_t)a.d * nk * 2 < (1ll << 31) && (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) &&
+  const int dm = max(a.d, a.v_d);
+  return dm > 32 && dm <= 128 && (nk % 8 == 0) && nk > 0 &&
+         (int64_t)dm * nk * 2 < (1ll << 31) && (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) &&
          (reinterpret_cast<uintptr_t>(a.V) % 16 == 0) && rule_is_interval(a.rule) &&
          a.b * ((a.rule.q.n + 127) / 128) < (1ll << 31);
 }
@@ -474,7 +481,8 @@ bool fwd_f16_fast_supported(const FwdArgs& a) {
 hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
   // FA_FWD_VARIANT = 1<NW><F>: e.g. 186 = 8 waves, flags 6 (timing runs); unset -> tuned default
   const int v = fast_variant();
-  if (a.d == 64 && v == 1899) {  // ablations (timing only)
+  const bool d64 = max(a.d, a.v_d) <= 64;
+  if (d64 && v == 1899) {  // ablations (timing only)
     const char* e = getenv("FA_FWD_ABL");
     switch (e ? atoi(e) : 0) {
       case 64: return launch_fast_t<64, 8, 6 | 64>(a, s);
@@ -488,7 +496,7 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
       default: return launch_fast_t<64, 8, 6>(a, s);
     }
   }
-  if (a.d == 64) {
+  if (d64) {
     switch (v) {
       case 180: return launch_fast_t<64, 8, 0>(a, s);
       case 182: return launch_fast_t<64, 8, 2>(a, s);
