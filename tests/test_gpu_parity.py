@@ -180,7 +180,7 @@ def test_reference_matrix(dtype, seq_dims, case):
 
 
 # ------------------------------------------------- small windows / strides
-@pytest.mark.parametrize("dtype", [np.float16, np.float32], ids=lambda t: np.dtype(t).name)
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
 @pytest.mark.parametrize("seq_dims,qs,ks", [(1, (300,), (300,)), (1, (257,), (130,)), (1, (130,), (517,)),
                                             (2, (12, 13), (12, 13)), (2, (16, 8), (8, 16))])
 @pytest.mark.parametrize("ws,ls,causal", [(1, 0, False), (2, 0, False), (8, 0, True), (37, 0, False), (2, 1, True),
@@ -228,8 +228,16 @@ def test_f32_mfma_shapes(d, policy, nq, nk):
     run_case(np.float32, policy, 1, "scale_end", (2, 1), d, d, (nq,), (nk,), ws=41, ls=0, causal=True, seed=d + 1)
 
 
+# fp64 MFMA path (fa_f64.hip): forward any d, v_d <= 128, backward d, v_d <= 64 (generic above)
+@pytest.mark.parametrize("d", [16, 32, 48, 64, 96, 128])
+@pytest.mark.parametrize("policy", ["full", "causal", "local"])
+@pytest.mark.parametrize("nq,nk", [(256, 256), (130, 1001)])
+def test_f64_mfma_shapes(d, policy, nq, nk):
+    run_case(np.float64, policy, 1, "scale_front", (2, 1), d, d, (nq,), (nk,), ws=41, ls=0, causal=True, seed=d + 2)
+
+
 # 1d local bands at MFMA sizes: the interval-rule path (per-lane key interval, empty tiles skipped)
-@pytest.mark.parametrize("dtype", [np.float16, np.float32], ids=lambda t: np.dtype(t).name)
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
 @pytest.mark.parametrize("ws,causal", [(64, False), (100, True), (256, False), (300, True)])
 @pytest.mark.parametrize("mode,nq,nk", [("none_front", 1500, 1500), ("scale_front", 700, 1500),
                                         ("scale_end", 1500, 600)])

@@ -172,6 +172,8 @@ int fa_forward(void* stream, const fa_problem* p, const void* Q, const void* K, 
     e = fa::launch_fwd_f16(a, s);
   } else if (p->dtype == FA_F32 && fa::fwd_f32_supported(a)) {
     e = fa::launch_fwd_f32(a, s);
+  } else if (p->dtype == FA_F64 && fa::fwd_f64_supported(a)) {
+    e = fa::launch_fwd_f64(a, s);
   } else {
     if (p->d > fa::generic_max_channels(p->dtype) || p->v_d > fa::generic_max_channels(p->dtype))
       return set_error(FA_ERR_UNSUPPORTED, "channel dimension exceeds the supported maximum for this dtype");
@@ -218,6 +220,8 @@ int fa_backward(void* stream, const fa_problem* p, const void* Q, const void* K,
     e = fa::launch_bwd_f16(a, s);
   } else if (p->dtype == FA_F32 && fa::bwd_f32_supported(a)) {
     e = fa::launch_bwd_f32(a, s);
+  } else if (p->dtype == FA_F64 && fa::bwd_f64_supported(a)) {
+    e = fa::launch_bwd_f64(a, s);
   } else {
     if (p->d > fa::generic_max_channels(p->dtype) || p->v_d > fa::generic_max_channels(p->dtype))
       return set_error(FA_ERR_UNSUPPORTED, "channel dimension exceeds the supported maximum for this dtype");
@@ -294,7 +298,7 @@ const char* fa_error_string(int status) {
 const char* fa_last_error(void) { return g_last_error.c_str(); }
 
 const char* fa_build_info(void) {
-  return "tf_flash_attention_amd: gfx950; fwd={mfma_f16, mfma_f32, generic(f16,f32,f64)}; bwd={mfma_f16 (two-pass / single-pass), mfma_f32 (two-pass), generic(f16,f32,f64)}";
+  return "tf_flash_attention_amd: gfx950; fwd={mfma_f16, mfma_f32, mfma_f64, generic(f16,f32,f64)}; bwd={mfma_f16 (two-pass / single-pass), mfma_f32 (two-pass), mfma_f64 (two-pass, d<=64), generic(f16,f32,f64)}";
 }
 
 }  // extern "C"

@@ -63,6 +63,11 @@ hipError_t launch_fwd_f32(const FwdArgs& a, hipStream_t s);
 bool bwd_f32_supported(const BwdArgs& a);
 hipError_t launch_bwd_f32(const BwdArgs& a, hipStream_t s);
 hipError_t launch_bwd_f16(const BwdArgs& a, hipStream_t s);
+// fp64 MFMA forward (d, v_d <= 128) and two-pass backward (d, v_d <= 64) — fa_f64.hip
+bool fwd_f64_supported(const FwdArgs& a);
+hipError_t launch_fwd_f64(const FwdArgs& a, hipStream_t s);
+bool bwd_f64_supported(const BwdArgs& a);
+hipError_t launch_bwd_f64(const BwdArgs& a, hipStream_t s);
 // two-pass fp16 backward (dK/dV key-outer + dQ query-outer, no atomics) — fa_bwd_f16_fast.hip
 bool bwd_f16_fast_supported(const BwdArgs& a);
 hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s);
