@@ -1,5 +1,6 @@
 // fa_bwd_f16_fast.hip — fp16 fused attention backward on gfx950 MFMA for the
-// common shapes (d == v_d ∈ {64, 128}, 16-byte aligned rows, nq % 8 == nk % 8 == 0)
+// common shapes (32 < max(d, v_d) <= 128, channels zero-padded to D ∈ {64, 128};
+// 16-byte aligned rows, nq % 8 == nk % 8 == 0)
 // under the full policy and the interval rules (causal, 1d unit-stride local).
 //
 // Replaces the reference's BackwardImpl (flash_attention.cu:1079-1967), which ran

@@ -1,6 +1,7 @@
 // fa_fwd_f16_fast.hip — fp16 fused attention forward, streamlined main loop for
-// the common shapes (d == v_d ∈ {64, 128}, K/V rows 16-byte aligned, nk % 8 == 0)
-// under the full policy and the interval rules (causal, 1d unit-stride local).
+// the common shapes (32 < max(d, v_d) <= 128, channels zero-padded to D ∈ {64, 128};
+// K/V rows 16-byte aligned, nk % 8 == 0) under the full policy and the interval
+// rules (causal, 1d unit-stride local).
 //
 // Same algorithm and operand layouts as fa_fwd_f16.hip (which remains the path
 // for every other shape and for strided / 2d local rules); what differs is how
