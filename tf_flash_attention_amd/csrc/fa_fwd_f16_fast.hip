@@ -483,6 +483,8 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
   // FA_FWD_VARIANT = 1<NW><F>: e.g. 186 = 8 waves, flags 6 (timing runs); unset -> tuned default
   const int v = fast_variant();
   const bool d64 = max(a.d, a.v_d) <= 64;
+  // paired-block kernel (one wave per SIMD): FA_FWD_VARIANT=2000 selects it for every rule it takes
+  if (fwd_f16_pp_supported(a) && v >= 2000 && v < 2200) return launch_fwd_f16_pp(a, s);
   if (d64 && v == 1899) {  // ablations (timing only)
     const char* e = getenv("FA_FWD_ABL");
     switch (e ? atoi(e) : 0) {

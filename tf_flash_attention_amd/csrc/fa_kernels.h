@@ -55,6 +55,9 @@ hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s);
 // streamlined fp16 forward for d == v_d in {64, 128} under full / interval rules — fa_fwd_f16_fast.hip
 bool fwd_f16_fast_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s);
+// paired-block fp16 forward for 32 < max(d, v_d) <= 64 (one wave per SIMD) — fa_fwd_f16_pp.hip
+bool fwd_f16_pp_supported(const FwdArgs& a);
+hipError_t launch_fwd_f16_pp(const FwdArgs& a, hipStream_t s);
 bool bwd_f16_supported(const BwdArgs& a);
 // fp32 MFMA forward — fa_fwd_f32.hip
 bool fwd_f32_supported(const FwdArgs& a);

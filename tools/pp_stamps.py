@@ -1,0 +1,41 @@
+"""Phase shares of the paired-block forward's key-loop step from its stamp build
+(FA_FWD_VARIANT=2132): per-wave s_memtime sums written over l.  Usage: python tools/pp_stamps.py [config]"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tf_flash_attention_amd import flash_attention as fa  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    cfgname = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, _ = bench.CONFIGS[cfgname]
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(1234)
+    b = int(np.prod(batch))
+    q = (torch.rand((b, d) + qs, generator=g, device=dev) * 4 - 2).to(dt)
+    k = (torch.rand((b, d) + ks, generator=g, device=dev) * 4 - 2).to(dt)
+    v = (torch.rand((b, d) + ks, generator=g, device=dev) * 4 - 2).to(dt)
+    os.environ["FA_FWD_VARIANT"] = sys.argv[2] if len(sys.argv) > 2 else "2132"
+    for _ in range(5):
+        o, l, m = fa.attention_forward(policy, seq_dims, q, k, v, sync, ws, ls, causal)
+    torch.cuda.synchronize()
+    nq = int(np.prod(qs))
+    lw = l.reshape(b, nq // 64, 64)[:, :, :6].float().cpu().numpy().reshape(-1, 6)
+    tot = lw.sum(axis=1, keepdims=True)
+    share = (lw / tot).mean(axis=0)
+    names = ["barrier", "stores+loads", "seg1 qk/max/rebase", "seg1 qk/exp/pv", "seg2 qk/max/rebase",
+             "seg2 qk/exp/pv/frag reads"]
+    nt = int(np.prod(ks)) // 64
+    print(json.dumps({"config": cfgname, "mean_cycles_per_wave": float(tot.mean()),
+                      "cycles_per_step": float(tot.mean()) / nt,
+                      "share": {n: round(float(x), 4) for n, x in zip(names, share)}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
