@@ -485,6 +485,11 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
   const bool d64 = max(a.d, a.v_d) <= 64;
   // paired-block kernel (one wave per SIMD): FA_FWD_VARIANT=2000 selects it for every rule it takes
   if (fwd_f16_pp_supported(a) && v >= 2000 && v < 2200) return launch_fwd_f16_pp(a, s);
+  // ping-pong kernel (two wave groups alternating MFMA / softmax phases): the default for
+  // d <= 64 under the full policy (c2: 948 vs 904 TF/s for the 8-wave kernel below);
+  // FA_FWD_VARIANT=22xx forces it (and its variants) for every rule it takes
+  if (fwd_f16_pingpong_supported(a) && ((v < 0 && a.rule.policy == 0) || (v >= 2200 && v < 2300)))
+    return launch_fwd_f16_pingpong(a, s);
   if (d64 && v == 1899) {  // ablations (timing only)
     const char* e = getenv("FA_FWD_ABL");
     switch (e ? atoi(e) : 0) {

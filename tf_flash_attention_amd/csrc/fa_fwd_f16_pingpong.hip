@@ -1,0 +1,429 @@
+// fa_fwd_f16_pingpong.hip — fp16 fused attention forward for 32 < max(d, v_d) <= 64,
+// full policy and interval rules: eight waves (two per SIMD) in two groups that
+// alternate MFMA and softmax phases ("ping-pong").
+//
+// At d = 64 a 32-query × 64-key tile is 16 MFMAs (512 matrix cycles) against ≈ 470
+// cycles of VALU / transcendental issue.  One wave cannot overlap the two (its softmax
+// depends on its own Sᵀ), and two free-running waves on a SIMD phase-lock behind the
+// workgroup barrier so their MFMA and softmax phases collide.  Here the workgroup
+// barrier itself keeps them apart: waves 0-3 (group 0) and waves 4-7 (group 1) share
+// the four SIMDs, and every barrier interval is an MFMA phase for one group and a
+// VALU phase for the other:
+//
+//   interval  2i  : group 0 MFMA(i)      | group 1 VALU(i-1)
+//   interval 2i+1 : group 0 VALU(i)      | group 1 MFMA(i)
+//
+// (both groups run the same loop; group 1 enters it one barrier late)
+//
+//   MFMA(i) = Sᵀ MFMAs of tile i + PV MFMAs of tile i-1 (16 MFMAs), beside all of the
+//             wave's LDS traffic: K(i+1) / V(i) fragment reads, its share of the staging
+//   VALU(i) = softmax of tile i (mask, max, speculative exp2, rare rebase, row sums)
+//
+// K/V tiles move global → registers (three steps ahead) → LDS; each thread owns one 16-B
+// chunk of every tile and stores it in its own MFMA phase, so a tile is complete and
+// published after the barrier that ends the second group's MFMA phase.  LDS images and
+// operand layouts are those of fa_fwd_f16_pp.hip (K: transposed reads with the key
+// permutation that makes P's k-step registers contiguous keys; V: plain rows, chunks
+// XOR-swizzled by (c>>1)&7).  Rings of three slots for K and V.
+//
+// Numerics as fa_fwd_f16.hip (fp32 accumulation, log2-domain lazy rebase at 8, l
+// relative to the stored fp16 m).  Replaces the reference's ForwardImpl
+// (flash_attention.cu:425-1077) for these shapes.
+#include "fa_device.h"
+#include "fa_kernels.h"
+#include "fa_mfma.h"
+
+#include <stdlib.h>
+
+namespace fa {
+namespace {
+
+using namespace mf;
+
+constexpr int kD = 64;
+constexpr int kBN = 64;              // keys per tile
+constexpr int kNW = 8;               // waves per workgroup, two per SIMD
+constexpr int kBM = 32 * kNW;        // queries per workgroup
+constexpr int kNS = 3;               // ring slots for K and for V
+constexpr int kQRow = 2 * kBM;       // bytes per Q row in LDS
+constexpr int kTile = kD * kBN * 2;  // 8 KB
+constexpr int kOffK = kD * kQRow;    // Q image [64][256] first (prologue only)
+constexpr int kOffV = kOffK + kNS * kTile;
+constexpr int kSmem = kOffV + kNS * kTile;
+constexpr float kRescaleThr = 8.f;
+
+// structure flags (FA_FWD_VARIANT=22xx selects them for A/B timing)
+constexpr int kFPrio = 1;  // s_setprio 1 over each MFMA phase
+constexpr int kFStamp = 2;  // diagnostic: per-wave s_memtime sums per phase part, written over l (l garbage)
+
+template <int POL, int F>
+__global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char_t* smem = (lds_char_t*)smem_raw;
+  constexpr float kNegInf = -__builtin_huge_valf();
+
+  const int nq = a.rule.q.n, nk = a.rule.k.n;
+  const uint32_t nqb = (nq + kBM - 1) / kBM;
+  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t bi = bid / nqb;
+  const int q0 = (int)(nqb - 1 - (bid % nqb)) * kBM;  // latest (heaviest under causal) blocks first
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = w >> 2;  // waves w and w+4 share a SIMD
+  const int h = lane >> 5, r = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+
+  const int d = a.d, vd = a.v_d;
+  const __half* Q = static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq;
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + bi * (int64_t)d * nk, 2u * d * nk);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk, 2u * vd * nk);
+  const bool qvec = ((nq & 7) == 0) && ((reinterpret_cast<uintptr_t>(a.Q) & 15) == 0);
+  const float c2 = (float)a.scale * kLog2e;
+
+  // ---- key range of the workgroup (rule-bounded)
+  const int qlast = min(q0 + kBM, nq) - 1;
+  int kb = 0, ke = nk;
+  if (POL != 0) k_range_for_q_block(a.rule, q0, qlast, &kb, &ke);
+  const int kt0 = (kb / kBN) * kBN;
+  const int ntiles = (ke > kb) ? (ke - kt0 + kBN - 1) / kBN : 0;
+
+  // ---- staging: this thread owns chunk `tid` of every tile = 8 keys (16 B) of channel row c
+  const int cm = tid & 7, crow = tid >> 3;
+  const uint32_t goff = (uint32_t)crow * (uint32_t)nk * 2u + 16u * cm;
+  const uint32_t koff = crow < d ? goff : 0x80000000u, voff = crow < vd ? goff : 0x80000000u;
+  const uint32_t kwo = crow * 128 + ((cm * 16) ^ ((crow & 2) << 5));
+  const uint32_t vwo = crow * 128 + 16 * (cm ^ ((crow >> 1) & 7));
+  // branch-free (exact vmcnt waits): chunks past nk — the tail, tiles past the end — read as zeros
+  auto load = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, int k0) -> u32x4 __attribute__((always_inline)) {
+    const bool in = k0 + 8 * cm < nk;
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off : 0x80000000u, 2 * min(k0, nk), 0);
+  };
+  auto store = [&](int off, u32x4 v) __attribute__((always_inline)) { *reinterpret_cast<lds_u32x4_t*>(smem + off) = v; };
+
+  // ---- prologue: Q, K(0..2), V(0..1) into LDS; K(3..5), V(2..4) into the staging registers
+  // (set j serves MFMA(i) with i mod 3 == j; loads run three steps ahead of their store)
+  u32x4 kst[kNS], vst[kNS];
+  {
+    u32x4 kp[3], vp[2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) kp[j] = load(krs, koff, kt0 + j * kBN);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) vp[j] = load(vrs, voff, kt0 + j * kBN);
+    for (int idx = tid; idx < kD * (kBM / 8); idx += kNW * 64) {  // Q [64][256], 64-B blocks XOR-swizzled by c&3
+      const int c = idx / (kBM / 8), m = idx % (kBM / 8);
+      const u32x4 v = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec) : u32x4{0, 0, 0, 0};
+      *reinterpret_cast<lds_u32x4_t*>(smem + c * kQRow + ((m * 16) ^ ((c & 3) << 6))) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) store(kOffK + j * kTile + kwo, kp[j]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) store(kOffV + j * kTile + vwo, vp[j]);
+#pragma unroll
+    for (int j = 0; j < kNS; ++j) {
+      kst[j] = load(krs, koff, kt0 + (3 + j) * kBN);
+      vst[j] = load(vrs, voff, kt0 + (2 + j) * kBN);
+    }
+  }
+  __syncthreads();
+
+  // Q*scale*log2(e) as the B operand of Sᵀ = Kᵀ·Q: lane (r,h) holds Q[c = 16s + 8h + e][q = 32w + r]
+  half8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int cr = 16 * s + 8 * (g >> 1) + 4 * e + tq;
+      const int col = 32 * w + 16 * (g & 1) + 4 * tp;
+      const half4 t = tr_read(smem + cr * kQRow + ((col * 2) ^ ((cr & 3) << 6)));
+      if (e == 0) qf[s].lo = t; else qf[s].hi = t;
+    }
+    qf[s] = scale8(qf[s], c2);
+  }
+
+  const int wq0 = q0 + 32 * w;
+  const int qi = wq0 + r;
+  const bool wave_active = wq0 < nq;
+  // POL 1: this lane's allowed keys [klo, klo + kspan) and the wave's bounds on them
+  int klo = 0, kspan = 0, wlo_min = 0, wlo_max = 0, whi_min = 0, whi_max = 0;
+  if (POL == 1 && wave_active) {
+    int khi;
+    key_interval(a.rule, min(qi, nq - 1), &klo, &khi);
+    kspan = max(khi - klo + 1, 0);
+    const int last = min(31, nq - 1 - wq0);
+    wlo_min = __builtin_amdgcn_readfirstlane(klo);
+    whi_min = __builtin_amdgcn_readfirstlane(khi);
+    wlo_max = __builtin_amdgcn_readlane(klo, last);
+    whi_max = __builtin_amdgcn_readlane(khi, last);
+  }
+  // tile class for this wave: 0 no allowed pair (skipped), 1 mixed (masked), 2 all allowed
+  auto tcls = [&](int it) -> int __attribute__((always_inline)) {
+    if (it < 0 || it >= ntiles) return 0;
+    const int k0 = kt0 + it * kBN, k1 = k0 + kBN - 1;
+    if (POL == 0) return (k1 < nk) ? 2 : 1;
+    if (!wave_active || wlo_min > k1 || whi_max < k0) return 0;
+    return (wlo_max <= k0 && whi_min >= k1 && k1 < nk) ? 2 : 1;
+  };
+
+  // fragment read bases (lane constants)
+  //   K: lane 4q+p of a 16-lane group supplies channel row q, keys 4σ(p)..4σ(p)+3, σ swapping 1 and 2,
+  //      so register i of Sᵀ half t holds key 32t + 16(i>>3) + 8h + (i&7)
+  const int sig = ((tp & 1) << 1) | (tp >> 1);
+  uint32_t kbase[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    kbase[t] = (8 * (g >> 1) + tq) * 128 + (((32 * t + 16 * (g & 1) + 4 * sig) * 2) ^ ((tq & 2) << 5));
+  //   V: lane (r, h) reads chunk 2s+h of channel row 32u + r
+  uint32_t vbase[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) vbase[s] = r * 128 + 16 * ((2 * s + h) ^ ((r >> 1) & 7));
+
+  half8 kf[2][4];  // K fragments for the next Sᵀ
+  half8 vf[4][2];  // V fragments for the next PV
+  auto read_k = [&](int slot) __attribute__((always_inline)) {
+    const lds_char_t* p = smem + kOffK + slot * kTile;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        kf[t][s].lo = tr_read(p + kbase[t] + (16 * s) * 128);
+        kf[t][s].hi = tr_read(p + kbase[t] + (16 * s + 4) * 128);
+      }
+  };
+  auto read_v = [&](int slot) __attribute__((always_inline)) {
+    const lds_char_t* p = smem + kOffV + slot * kTile;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) vf[s][u] = read_b128(p + vbase[s] + 32 * u * 128);
+  };
+
+  floatx16 st[2];      // Sᵀ of the tile being softmaxed
+  uint32_t pw[4][4];   // P (fp16 pairs), dword x of PV k-step s (dwords: extracting them from a
+                       // bit-cast half8 miscompiles with this toolchain)
+  floatx16 o[2];       // Oᵀ: channels 32u + 8(i>>2) + 4h + (i&3)
+  floatx16 negm;       // -m_run broadcast: the C operand of every Sᵀ chain
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.f;
+    o[1][i] = 0.f;
+    negm[i] = 0.f;
+  }
+  float m_run = 0.f, l0 = 0.f, l1 = 0.f, m_max = kNegInf, thr = -__FLT_MAX__;
+
+  auto mask = [&](int k0) __attribute__((always_inline)) {
+    const int lim = nk - k0 - 8 * h;       // POL 0: offset o is in range iff o < lim
+    const int base = k0 + 8 * h - klo;     // POL 1: allowed iff base + o in [0, kspan)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int off = 32 * t + 16 * (i >> 3) + (i & 7);
+        const bool ok = (POL == 1) ? ((unsigned)(base + off) < (unsigned)kspan) : (off < lim);
+        st[t][i] = ok ? st[t][i] : kNegInf;
+      }
+  };
+  auto exp_cvt = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const float s0 = st[s >> 1][8 * (s & 1) + 2 * x], s1 = st[s >> 1][8 * (s & 1) + 2 * x + 1];
+        pw[s][x] = __builtin_bit_cast(uint32_t, half2v{(_Float16)__builtin_amdgcn_exp2f(s0),
+                                                       (_Float16)__builtin_amdgcn_exp2f(s1)});
+      }
+  };
+  // softmax of tile `it`: the exponentials are computed speculatively against m_run beside the
+  // row max; only a seed or a max past the threshold (rare) rebases O, l, Sᵀ, -m and redoes them
+  auto softmax = [&](int it, int cls) __attribute__((always_inline)) {
+    if (cls == 1) mask(kt0 + it * kBN);
+    // four independent max3 chains (one wave does the VALU work on its SIMD: latency shows)
+    float mx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mx[j] = fmaxf(st[j >> 1][8 * (j & 1)], st[j >> 1][8 * (j & 1) + 1]);
+#pragma unroll
+    for (int i = 2; i < 8; i += 2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        mx[j] = fmaxf(fmaxf(mx[j], st[j >> 1][8 * (j & 1) + i]), st[j >> 1][8 * (j & 1) + i + 1]);
+    const float mt = max_pair32(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
+    m_max = fmaxf(m_max, m_run + mt);
+    exp_cvt();
+#pragma unroll
+    for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
+      asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
+    if (__any(mt > thr)) {
+      const bool unset = thr < 0.f;
+      const bool seed = unset && (mt > thr);
+      const float delta = unset ? (seed ? mt : 0.f) : fmaxf(mt, 0.f);
+      const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
+      m_run += delta;
+      thr = (unset && !seed) ? thr : kRescaleThr;
+      l0 *= alpha;
+      l1 *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o[0][i] *= alpha;
+        o[1][i] *= alpha;
+        st[0][i] -= delta;
+        st[1][i] -= delta;
+        negm[i] = -m_run;
+      }
+      exp_cvt();
+    }
+    const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
+    float ls[4] = {0.f, 0.f, 0.f, 0.f};  // four chains, folded into l0 / l1 once
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) ls[x] = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2v, pw[s][x]), one2, ls[x], false);
+    l0 += ls[0] + ls[2];
+    l1 += ls[1] + ls[3];
+  };
+
+  // MFMA(i): this wave's chunks of K(i+3) / V(i+2) into LDS (over K(i) / V(i-1), whose
+  // fragments were read in MFMA(i-1)), loads of K(i+6) / V(i+5); Sᵀ of tile i; K(i+1)
+  // fragments; PV of tile i-1 (P from VALU(i-1)); V(i) fragments.  The LDS traffic sits in the
+  // MFMA phase, beside the matrix pipe, so the VALU phase is the softmax alone.
+  auto mfma_phase = [&](auto C_, int it) __attribute__((always_inline)) {
+    constexpr int c = decltype(C_)::value;  // it mod 3
+    if (F & kFPrio) __builtin_amdgcn_s_setprio(1);
+    // (unconditional: past the end these move zeros into slots nobody reads unmasked)
+    store(kOffK + c * kTile + kwo, kst[c]);
+    store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
+    kst[c] = load(krs, koff, kt0 + (it + 6) * kBN);
+    vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
+    if (tcls(it) != 0) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], qf[s], s == 0 ? negm : st[t], 0, 0, 0);
+    }
+    read_k((c + 1) % kNS);
+    if (tcls(it - 1) != 0) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const half8 p = __builtin_bit_cast(half8, u32x4{pw[s][0], pw[s][1], pw[s][2], pw[s][3]});
+#pragma unroll
+        for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[u], 0, 0, 0);
+      }
+    }
+    read_v(c);
+    // No lgkmcnt drain here: a wave's LDS operations complete in order, and each wave waits for
+    // its fragment reads before the MFMAs that use them (MFMA(i+1)), which orders its stores of
+    // this phase before any other wave reads those tiles (MFMA(i+2)) and its reads before any
+    // wave overwrites their slots (MFMA(i+1) for itself, one interval later for the others).
+    if (F & kFPrio) __builtin_amdgcn_s_setprio(0);
+  };
+  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if constexpr ((F & kFStamp) != 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      uint64_t t;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (k >= 0) st_acc[k] += t - st_prev;
+      st_prev = t;
+    }
+  };
+  // VALU(i): the softmax of tile i
+  auto valu_phase = [&](int it) __attribute__((always_inline)) {
+    const int cls = tcls(it);
+    stamp(3);
+    if (cls != 0) softmax(it, cls);
+    stamp(4);
+    stamp(5);
+  };
+
+  // Both groups run the same loop (one code path keeps the register allocation sane); group 1
+  // enters it one barrier late and group 0 leaves it one barrier late, so every barrier
+  // interval pairs one group's MFMA(i) with the other's VALU phase.
+  read_k(0);
+  if (grp == 1) __builtin_amdgcn_s_barrier();
+  auto iter = [&](auto C_, int it) __attribute__((always_inline)) {
+    stamp(-1);
+    __builtin_amdgcn_s_barrier();
+    stamp(0);
+    mfma_phase(C_, it);
+    stamp(1);
+    __builtin_amdgcn_s_barrier();
+    stamp(2);
+    valu_phase(it);
+  };
+  // Whole groups of three iterations, none conditional (the last ones past the end only move
+  // zeros): with no control flow around the staging loads, hipcc's vmcnt waits stay exact and
+  // a store waits only for the load issued three steps earlier.
+  for (int it = 0; it <= ntiles; it += kNS) {
+    iter(IC<0>{}, it);
+    iter(IC<1>{}, it + 1);
+    iter(IC<2>{}, it + 2);
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();
+
+  // ---- epilogue
+  if (!wave_active) return;
+  const float l_tot = sum_pair32(l0 + l1);
+  const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
+  if (qi >= nq) return;
+  __half* O = static_cast<__half*>(a.O) + bi * (int64_t)vd * nq;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int v = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (v < vd) O[(int64_t)v * nq + qi] = __float2half(o[u][i] * inv);
+    }
+  if (h == 0) {
+    float* lo = static_cast<float*>(a.l) + bi * (int64_t)nq;
+    __half* mo = static_cast<__half*>(a.m) + bi * (int64_t)nq;
+    if (l_tot > 0.f) {
+      const __half mT = __float2half(m_max * kLn2);
+      // l relative to the STORED (rounded) m, so exp(s - m)/l is exact downstream
+      lo[qi] = l_tot * __builtin_amdgcn_exp2f(m_run - __half2float(mT) * kLog2e);
+      mo[qi] = mT;
+    } else {
+      lo[qi] = 0.f;
+      mo[qi] = neg_inf_approx<__half>();
+    }
+  }
+  if constexpr ((F & kFStamp) != 0) {  // diagnostic build: stamps over this wave's first l entries
+    if (lane < 6) {
+      uint64_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v = (lane == k) ? st_acc[k] : v;
+      static_cast<float*>(a.l)[bi * (int64_t)nq + wq0 + lane] = (float)v;
+    }
+  }
+}
+
+template <int F>
+hipError_t launch_t(const FwdArgs& a, hipStream_t s) {
+  const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
+  auto kern = a.rule.policy == 0 ? fwd_f16_pingpong_kernel<0, F> : fwd_f16_pingpong_kernel<1, F>;
+  hipError_t e =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kNW * 64), kSmem, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool fwd_f16_pingpong_supported(const FwdArgs& a) {
+  const int nk = a.rule.k.n;
+  const int dm = max(a.d, a.v_d);
+  return dm > 32 && dm <= kD && (nk % 8 == 0) && nk > 0 && (int64_t)dm * nk * 2 < (1ll << 31) &&
+         (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) && (reinterpret_cast<uintptr_t>(a.V) % 16 == 0) &&
+         rule_is_interval(a.rule) && a.b * ((a.rule.q.n + kBM - 1) / kBM) < (1ll << 31);
+}
+
+hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
+  const char* ev = getenv("FA_FWD_VARIANT");
+  switch (ev ? atoi(ev) : -1) {
+    case 2200: return launch_t<0>(a, s);
+    case 2203: return launch_t<kFPrio | kFStamp>(a, s);
+    default: return launch_t<kFPrio>(a, s);  // tuned (c2, MI355X): MFMA phases at priority 1
+  }
+}
+
+}  // namespace fa

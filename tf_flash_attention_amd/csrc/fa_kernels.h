@@ -58,6 +58,9 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s);
 // paired-block fp16 forward for 32 < max(d, v_d) <= 64 (one wave per SIMD) — fa_fwd_f16_pp.hip
 bool fwd_f16_pp_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_pp(const FwdArgs& a, hipStream_t s);
+// ping-pong fp16 forward (8 waves, two groups alternating MFMA / softmax phases) — fa_fwd_f16_pingpong.hip
+bool fwd_f16_pingpong_supported(const FwdArgs& a);
+hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s);
 bool bwd_f16_supported(const BwdArgs& a);
 // fp32 MFMA forward — fa_fwd_f32.hip
 bool fwd_f32_supported(const FwdArgs& a);

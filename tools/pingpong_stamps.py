@@ -1,0 +1,39 @@
+"""Phase breakdown of the ping-pong forward from its stamp build (FA_FWD_VARIANT=2203):
+per-wave s_memtime sums written over l, split by wave group.  Usage: python tools/pingpong_stamps.py [config]"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tf_flash_attention_amd import flash_attention as fa  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    cfgname = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, _ = bench.CONFIGS[cfgname]
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(1234)
+    b = int(np.prod(batch))
+    q = (torch.rand((b, d) + qs, generator=g, device=dev) * 4 - 2).to(dt)
+    k = (torch.rand((b, d) + ks, generator=g, device=dev) * 4 - 2).to(dt)
+    v = (torch.rand((b, d) + ks, generator=g, device=dev) * 4 - 2).to(dt)
+    os.environ["FA_FWD_VARIANT"] = sys.argv[2] if len(sys.argv) > 2 else "2203"
+    for _ in range(5):
+        o, l, m = fa.attention_forward(policy, seq_dims, q, k, v, sync, ws, ls, causal)
+    torch.cuda.synchronize()
+    nq = int(np.prod(qs))
+    lw = l.reshape(b, nq // 256, 8, 32)[:, :, :, :6].float().cpu().numpy()  # [b, blocks, wave, part]
+    nt = int(np.prod(ks)) // 64
+    names = ["barrier before MFMA", "MFMA phase", "barrier before VALU", "stores+loads", "softmax", "frag reads+wait"]
+    for grp in (0, 1):
+        x = lw[:, :, 4 * grp:4 * grp + 4, :].reshape(-1, 6).mean(axis=0) / nt
+        print(json.dumps({"config": cfgname, "group": grp, "cycles_per_step": round(float(x.sum()), 1),
+                          "parts": {n: round(float(v), 1) for n, v in zip(names, x)}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
