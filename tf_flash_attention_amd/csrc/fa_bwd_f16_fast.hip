@@ -93,7 +93,7 @@ __device__ __forceinline__ void g_store(lds_char_t* img, int c, int m, u32x4 v) 
   *reinterpret_cast<lds_u32x2_t*>(p + (D + kGPad) * 16) = v.zw;
 }
 
-template <int D, int NW>
+template <int D, int NW, int NS = 2>
 struct DkdvSmem {
   static constexpr int kBK = 32 * NW;                 // keys per workgroup
   static constexpr int kRow = D * kBK * 2;            // K (or V) row image
@@ -101,17 +101,22 @@ struct DkdvSmem {
   static constexpr int kG = 4 * (D + kGPad) * 16;     // one 32-column G image
   static constexpr int offQT = 0, offOT = kQT, offQG = 2 * kQT, offOG = 2 * kQT + kG, offLse = 2 * kQT + 2 * kG;
   static constexpr int kSlot = offLse + 2 * 32 * 4;   // + lse2[32], D[32]
-  static constexpr int kRing = 2 * kSlot;
+  static constexpr int kRing = NS * kSlot;
   static constexpr int kTotal = (kRing > 2 * kRow) ? kRing : 2 * kRow;  // the K/V images alias the ring
 };
 
 // ---------------------------------------------------------------------------
-// dK / dV: key-outer.  One workgroup = NW waves x 32 keys of one (batch, head) slice.
-template <int D, int NW, int WPE, int POL>
+// dK / dV: key-outer.
+// PIPE (one wave per SIMD, registers to spare): software-pipelined over query tiles with a
+// 3-slot ring — the S / dP MFMAs of tile it+1 are issued beside the softmax of tile it, then
+// the dV / dK MFMAs of tile it; the LDS latency of one tile's operand reads and the VALU
+// work hide under the other tile's MFMAs (a single wave per SIMD has nothing else to hide
+// them behind).  One workgroup = NW waves x 32 keys of one (batch, head) slice.
+template <int D, int NW, int WPE, int POL, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
-  using S = DkdvSmem<D, NW>;
+  using S = DkdvSmem<D, NW, PIPE ? 3 : 2>;
   constexpr int kThr = NW * 64;
   constexpr int kBK = S::kBK;
   constexpr int kQChunks = D * 4;                     // 16-B chunks of one [D][32] tile
@@ -242,22 +247,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) { dk[u][i] = 0.f; dv[u][i] = 0.f; }
 
-  if (ntiles > 0) { load_tile(qt0); store_tile(0); }
-  if (ntiles > 1) load_tile(qt0 + 32);
-
-  // iteration it: tile it in slot it&1 (complete after the barrier); tile it+1 -> slot (it+1)&1
-  // (read in iteration it-1, finished before this barrier); tile it+2 -> registers
-  auto step = [&](auto P_, int it) {
-    constexpr int p = decltype(P_)::value;
-    __syncthreads();
-    const int qa = qt0 + 32 * it;
-    if (it + 1 < ntiles) store_tile(p ^ 1);
-    if (it + 2 < ntiles) load_tile(qa + 64);
-    const int cls = tcls(qa);
-    if (cls == 0) return;
-    const lds_char_t* base = smem + p * S::kSlot;
-    // row constants as the initial accumulators: S: -lse2[q], dP: -D[q], q = (i&3) + 8(i>>2) + 4h
-    floatx16 sacc, pacc;
+  // row constants of the tile in `base` as initial accumulators: S: -lse2[q], dP: -D[q]
+  auto init_acc = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) {
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq) {
       const floatx4 l4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 4 * (8 * gq + 4 * h));
@@ -268,7 +259,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
         pacc[4 * gq + j] = -d4[j];
       }
     }
-    // S = Qᵀ·K', dP = dOᵀ·V: A operands (row q, k = channel) by transposed reads
+  };
+  // S = Qᵀ·K', dP = dOᵀ·V: A operands (row q, k = channel) by transposed reads
+  auto sdp = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) {
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
       half8 qa8, oa8;
@@ -281,8 +274,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8, kb[s], sacc, 0, 0, 0);
       pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8, vb[s], pacc, 0, 0, 0);
     }
-    // P = exp2(S), dS = P∘dP; k-step s of the dV / dK products = registers 8s..8s+7
-    half8 pf[2], sf[2];
+  };
+  // P = exp2(S), dS = P∘dP; k-step s of the dV / dK products = registers 8s..8s+7
+  auto softmax = [&](const floatx16& sacc, const floatx16& pacc, int qa, int cls, half8 (&pf)[2], half8 (&sf)[2]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float pv = __builtin_amdgcn_exp2f(sacc[i]);
@@ -293,7 +287,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       pf[i >> 3][i & 7] = (_Float16)pv;
       sf[i >> 3][i & 7] = (_Float16)(pv * pacc[i]);
     }
-    // dV += dO·P, dK += Q·dS: A = X[row 32u + r][group (s, h)] (G images)
+  };
+  // dV += dO·P, dK += Q·dS: A = X[row 32u + r][group (s, h)] (G images)
+  auto dvdk = [&](const lds_char_t* base, const half8 (&pf)[2], const half8 (&sf)[2]) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -304,9 +300,78 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
         dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa, sf[s], dk[u], 0, 0, 0);
       }
   };
-  for (int it = 0; it < ntiles; it += 2) {
-    step(IC<0>{}, it);
-    if (it + 1 < ntiles) step(IC<1>{}, it + 1);
+
+  if constexpr (!PIPE) {
+    if (ntiles > 0) { load_tile(qt0); store_tile(0); }
+    if (ntiles > 1) load_tile(qt0 + 32);
+
+    // iteration it: tile it in slot it&1 (complete after the barrier); tile it+1 -> slot (it+1)&1
+    // (read in iteration it-1, finished before this barrier); tile it+2 -> registers
+    auto step = [&](auto P_, int it) {
+      constexpr int p = decltype(P_)::value;
+      __syncthreads();
+      const int qa = qt0 + 32 * it;
+      if (it + 1 < ntiles) store_tile(p ^ 1);
+      if (it + 2 < ntiles) load_tile(qa + 64);
+      const int cls = tcls(qa);
+      if (cls == 0) return;
+      const lds_char_t* base = smem + p * S::kSlot;
+      floatx16 sacc, pacc;
+      init_acc(base, sacc, pacc);
+      sdp(base, sacc, pacc);
+      half8 pf[2], sf[2];
+      softmax(sacc, pacc, qa, cls, pf, sf);
+      dvdk(base, pf, sf);
+    };
+    for (int it = 0; it < ntiles; it += 2) {
+      step(IC<0>{}, it);
+      if (it + 1 < ntiles) step(IC<1>{}, it + 1);
+    }
+  } else {
+    // tile j lives in slot j % 3; step it: barrier (tile it+1 complete), tile it+2 -> slot
+    // (it+2)%3 (tile it-1's, finished in step it-1), tile it+3 -> registers; S/dP(it+1) beside
+    // the softmax of tile it; dV/dK(it)
+    if (ntiles > 0) { load_tile(qt0); store_tile(0); }
+    if (ntiles > 1) { load_tile(qt0 + 32); store_tile(1); }
+    if (ntiles > 2) load_tile(qt0 + 64);
+    __syncthreads();
+    floatx16 sa, pa, sb, pb;  // S / dP accumulators of two consecutive tiles
+    if (ntiles > 0 && tcls(qt0) != 0) {
+      init_acc(smem, sa, pa);
+      sdp(smem, sa, pa);
+    }
+    auto step = [&](auto C_, auto Q_, int it, floatx16& scur, floatx16& pcur, floatx16& snxt, floatx16& pnxt) {
+      constexpr int c = decltype(C_)::value;  // it mod 3
+      __syncthreads();
+      const int qa = qt0 + 32 * it;
+      if (it + 2 < ntiles) store_tile((c + 2) % 3);
+      if (it + 3 < ntiles) load_tile(qa + 96);
+      const int cls = tcls(qa);
+      const int cls1 = (it + 1 < ntiles) ? tcls(qa + 32) : 0;
+      const lds_char_t* base = smem + c * S::kSlot;
+      const lds_char_t* base1 = smem + ((c + 1) % 3) * S::kSlot;
+      half8 pf[2], sf[2];
+      if (cls1 != 0 && cls != 0) {  // one basic block: tile it+1's MFMAs beside tile it's softmax
+        init_acc(base1, snxt, pnxt);
+        sdp(base1, snxt, pnxt);
+        softmax(scur, pcur, qa, cls, pf, sf);
+      } else {
+        if (cls1 != 0) {
+          init_acc(base1, snxt, pnxt);
+          sdp(base1, snxt, pnxt);
+        }
+        if (cls != 0) softmax(scur, pcur, qa, cls, pf, sf);
+      }
+      if (cls != 0) dvdk(base, pf, sf);
+    };
+    for (int it = 0; it < ntiles; it += 6) {
+      step(IC<0>{}, IC<0>{}, it, sa, pa, sb, pb);
+      if (it + 1 < ntiles) step(IC<1>{}, IC<1>{}, it + 1, sb, pb, sa, pa);
+      if (it + 2 < ntiles) step(IC<2>{}, IC<0>{}, it + 2, sa, pa, sb, pb);
+      if (it + 3 < ntiles) step(IC<0>{}, IC<1>{}, it + 3, sb, pb, sa, pa);
+      if (it + 4 < ntiles) step(IC<1>{}, IC<0>{}, it + 4, sa, pa, sb, pb);
+      if (it + 5 < ntiles) step(IC<2>{}, IC<1>{}, it + 5, sb, pb, sa, pa);
+    }
   }
 
   // ---- dK = scale·Σ dS·Q, dV: rows c = 32u + (i&3) + 8(i>>2) + 4h, column = this lane's key
@@ -539,11 +604,11 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     }
 }
 
-template <int D, int NW, int WPE>
+template <int D, int NW, int WPE, bool PIPE = false>
 hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
-  using S = DkdvSmem<D, NW>;
+  using S = DkdvSmem<D, NW, PIPE ? 3 : 2>;
   const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
-  auto kern = a.rule.policy == 0 ? bwd_dkdv_kernel<D, NW, WPE, 0> : bwd_dkdv_kernel<D, NW, WPE, 1>;
+  auto kern = a.rule.policy == 0 ? bwd_dkdv_kernel<D, NW, WPE, 0, PIPE> : bwd_dkdv_kernel<D, NW, WPE, 1, PIPE>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      S::kTotal);
   if (e != hipSuccess) return e;
@@ -597,7 +662,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
       default: return launch_dq<64, 4, 2>(a, s);
     }
   }
-  e = launch_dkdv<128, 4, 1>(a, s);
+  e = (v == 1281) ? launch_dkdv<128, 4, 1, true>(a, s) : launch_dkdv<128, 4, 1>(a, s);
   if (e != hipSuccess) return e;
   return launch_dq<128, 4, 1>(a, s);
 }

@@ -54,7 +54,8 @@ constexpr float kRescaleThr = 8.f;
 
 // structure flags (FA_FWD_VARIANT=22xx selects them for A/B timing)
 constexpr int kFPrio = 1;  // s_setprio 1 over each MFMA phase
-constexpr int kFStamp = 2;  // diagnostic: per-wave s_memtime sums per phase part, written over l (l garbage)
+constexpr int kFStamp = 2;
+constexpr int kFSumsLate = 4;  // row sums of P(i-1) in MFMA(i) instead of VALU(i-1)  // diagnostic: per-wave s_memtime sums per phase part, written over l (l garbage)
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
@@ -222,6 +223,16 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         st[t][i] = ok ? st[t][i] : kNegInf;
       }
   };
+  auto row_sums = [&]() __attribute__((always_inline)) {
+    const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
+    float ls[4] = {0.f, 0.f, 0.f, 0.f};  // four chains, folded into l0 / l1 once
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) ls[x] = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2v, pw[s][x]), one2, ls[x], false);
+    l0 += ls[0] + ls[2];
+    l1 += ls[1] + ls[3];
+  };
   auto exp_cvt = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -270,14 +281,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
       }
       exp_cvt();
     }
-    const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
-    float ls[4] = {0.f, 0.f, 0.f, 0.f};  // four chains, folded into l0 / l1 once
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) ls[x] = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2v, pw[s][x]), one2, ls[x], false);
-    l0 += ls[0] + ls[2];
-    l1 += ls[1] + ls[3];
+    if (!(F & kFSumsLate)) row_sums();
   };
 
   // MFMA(i): this wave's chunks of K(i+3) / V(i+2) into LDS (over K(i) / V(i-1), whose
@@ -301,6 +305,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     }
     read_k((c + 1) % kNS);
     if (tcls(it - 1) != 0) {
+      if (F & kFSumsLate) row_sums();
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const half8 p = __builtin_bit_cast(half8, u32x4{pw[s][0], pw[s][1], pw[s][2], pw[s][3]});
@@ -422,6 +427,7 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
   switch (ev ? atoi(ev) : -1) {
     case 2200: return launch_t<0>(a, s);
     case 2203: return launch_t<kFPrio | kFStamp>(a, s);
+    case 2205: return launch_t<kFPrio | kFSumsLate>(a, s);
     default: return launch_t<kFPrio>(a, s);  // tuned (c2, MI355X): MFMA phases at priority 1
   }
 }

@@ -20,11 +20,11 @@ if [ "$1" == "--collect" ]; then   # local: keep the summaries, drop the raw tra
 fi
 export TMPDIR=/tmp
 mkdir -p $OUT
-declare -A REGEX=([c2]=fwd_f16_fast [c3]="fwd_f16_fast|bwd_dkdv|bwd_dq|bwd_prep" [c4]=fwd_f16_fast [c5]=fwd_f32_kernel)
+declare -A REGEX=([c2]=fwd_f16 [c3]="fwd_f16|bwd_dkdv|bwd_dq|bwd_prep" [c4]=fwd_f16 [c5]=fwd_f32_kernel)
 for cfg in ${CONFIGS:-c2}; do
   rx=${REGEX[$cfg]}
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$cfg -o run \
-      -- python3 bench.py --config $cfg --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof_$cfg.log 2>&1
+      -- python3 bench.py --config $cfg --no-cpu-baseline > $OUT/prof_$cfg.log 2>&1
   c=$?; echo "[$cfg] kernel-trace exit $c"; [ $c -eq 0 ] || exit $c
   cp "$(find $OUT/prof_$cfg -name '*kernel_stats.csv' | head -1)" $OUT/${cfg}_kernel_stats.csv
   grep -h '^{' $OUT/prof_$cfg.log > $OUT/${cfg}_bench_under_rocprof.json || true
