@@ -53,9 +53,11 @@ constexpr int kSmem = kOffV + kNS * kTile;
 constexpr float kRescaleThr = 8.f;
 
 // structure flags (FA_FWD_VARIANT=22xx selects them for A/B timing)
-constexpr int kFPrio = 1;  // s_setprio 1 over each MFMA phase
-constexpr int kFStamp = 2;
-constexpr int kFSumsLate = 4;  // row sums of P(i-1) in MFMA(i) instead of VALU(i-1)  // diagnostic: per-wave s_memtime sums per phase part, written over l (l garbage)
+constexpr int kFPrio = 1;      // s_setprio 1 over each MFMA phase (the default)
+constexpr int kFStamp = 2;     // diagnostic: per-wave s_memtime sums per phase part, written over l (l garbage)
+constexpr int kFSumsLate = 4;  // row sums of P(i-1) in MFMA(i) instead of VALU(i-1) (measured slower)
+// ablations (timing diagnostics, outputs WRONG): no exp2 (P = cvt(S)), no row max / rebase, no row sums
+constexpr int kANoExp = 8, kANoMax = 16, kANoSums = 32;
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
@@ -239,8 +241,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         const float s0 = st[s >> 1][8 * (s & 1) + 2 * x], s1 = st[s >> 1][8 * (s & 1) + 2 * x + 1];
-        pw[s][x] = __builtin_bit_cast(uint32_t, half2v{(_Float16)__builtin_amdgcn_exp2f(s0),
-                                                       (_Float16)__builtin_amdgcn_exp2f(s1)});
+        pw[s][x] = (F & kANoExp) ? __builtin_bit_cast(uint32_t, half2v{(_Float16)s0, (_Float16)s1})
+                                 : __builtin_bit_cast(uint32_t, half2v{(_Float16)__builtin_amdgcn_exp2f(s0),
+                                                                       (_Float16)__builtin_amdgcn_exp2f(s1)});
       }
   };
   // softmax of tile `it`: the exponentials are computed speculatively against m_run beside the
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         mx[j] = fmaxf(fmaxf(mx[j], st[j >> 1][8 * (j & 1) + i]), st[j >> 1][8 * (j & 1) + i + 1]);
-    const float mt = max_pair32(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
+    const float mt = (F & kANoMax) ? -1.f : max_pair32(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
     m_max = fmaxf(m_max, m_run + mt);
     exp_cvt();
 #pragma unroll
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
       }
       exp_cvt();
     }
-    if (!(F & kFSumsLate)) row_sums();
+    if (!(F & (kFSumsLate | kANoSums))) row_sums();
   };
 
   // MFMA(i): this wave's chunks of K(i+3) / V(i+2) into LDS (over K(i) / V(i-1), whose
@@ -428,6 +431,11 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2200: return launch_t<0>(a, s);
     case 2203: return launch_t<kFPrio | kFStamp>(a, s);
     case 2205: return launch_t<kFPrio | kFSumsLate>(a, s);
+    case 2211: return launch_t<kFPrio | kFStamp | kANoExp>(a, s);
+    case 2219: return launch_t<kFPrio | kFStamp | kANoMax>(a, s);
+    case 2235: return launch_t<kFPrio | kFStamp | kANoSums>(a, s);
+    case 2259: return launch_t<kFPrio | kFStamp | kANoExp | kANoMax | kANoSums>(a, s);
+    case 2260: return launch_t<kFPrio | kANoExp | kANoMax | kANoSums>(a, s);
     default: return launch_t<kFPrio>(a, s);  // tuned (c2, MI355X): MFMA phases at priority 1
   }
 }
