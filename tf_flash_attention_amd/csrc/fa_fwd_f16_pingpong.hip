@@ -58,6 +58,8 @@ constexpr int kFStamp = 2;     // diagnostic: per-wave s_memtime sums per phase 
 constexpr int kFSumsLate = 4;  // row sums of P(i-1) in MFMA(i) instead of VALU(i-1) (measured slower)
 // ablations (timing diagnostics, outputs WRONG): no exp2 (P = cvt(S)), no row max / rebase, no row sums
 constexpr int kANoExp = 8, kANoMax = 16, kANoSums = 32;
+// ... and in the MFMA phase: no staging loads, no LDS stores, no fragment reads
+constexpr int kANoLoad = 64, kANoStore = 128, kANoFrag = 256;
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
@@ -295,10 +297,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     constexpr int c = decltype(C_)::value;  // it mod 3
     if (F & kFPrio) __builtin_amdgcn_s_setprio(1);
     // (unconditional: past the end these move zeros into slots nobody reads unmasked)
-    store(kOffK + c * kTile + kwo, kst[c]);
-    store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
-    kst[c] = load(krs, koff, kt0 + (it + 6) * kBN);
-    vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
+    if (!(F & kANoStore)) {
+      store(kOffK + c * kTile + kwo, kst[c]);
+      store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
+    }
+    if (!(F & kANoLoad)) {
+      kst[c] = load(krs, koff, kt0 + (it + 6) * kBN);
+      vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
+    }
     if (tcls(it) != 0) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -306,7 +312,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         for (int t = 0; t < 2; ++t)
           st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], qf[s], s == 0 ? negm : st[t], 0, 0, 0);
     }
-    read_k((c + 1) % kNS);
+    if (!(F & kANoFrag)) read_k((c + 1) % kNS);
     if (tcls(it - 1) != 0) {
       if (F & kFSumsLate) row_sums();
 #pragma unroll
@@ -316,7 +322,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[u], 0, 0, 0);
       }
     }
-    read_v(c);
+    if (!(F & kANoFrag)) read_v(c);
     // No lgkmcnt drain here: a wave's LDS operations complete in order, and each wave waits for
     // its fragment reads before the MFMAs that use them (MFMA(i+1)), which orders its stores of
     // this phase before any other wave reads those tiles (MFMA(i+2)) and its reads before any
@@ -436,6 +442,11 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2235: return launch_t<kFPrio | kFStamp | kANoSums>(a, s);
     case 2259: return launch_t<kFPrio | kFStamp | kANoExp | kANoMax | kANoSums>(a, s);
     case 2260: return launch_t<kFPrio | kANoExp | kANoMax | kANoSums>(a, s);
+    case 2264: return launch_t<kFPrio | kANoLoad>(a, s);
+    case 2265: return launch_t<kFPrio | kANoStore>(a, s);
+    case 2266: return launch_t<kFPrio | kANoFrag>(a, s);
+    case 2267: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag>(a, s);
+    case 2268: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
     default: return launch_t<kFPrio>(a, s);  // tuned (c2, MI355X): MFMA phases at priority 1
   }
 }
