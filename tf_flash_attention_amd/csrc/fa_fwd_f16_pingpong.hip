@@ -44,12 +44,15 @@ constexpr int kD = 64;
 constexpr int kBN = 64;              // keys per tile
 constexpr int kNW = 8;               // waves per workgroup, two per SIMD
 constexpr int kBM = 32 * kNW;        // queries per workgroup
-constexpr int kNS = 3;               // ring slots for K and for V
 constexpr int kQRow = 2 * kBM;       // bytes per Q row in LDS
 constexpr int kTile = kD * kBN * 2;  // 8 KB
 constexpr int kOffK = kD * kQRow;    // Q image [64][256] first (prologue only)
-constexpr int kOffV = kOffK + kNS * kTile;
-constexpr int kSmem = kOffV + kNS * kTile;
+// ring slots for K and for V: 3 with register staging, 5 with LDS-DMA staging (kFDma)
+template <bool DMA> struct Ring {
+  static constexpr int kNS = DMA ? 5 : 3;
+  static constexpr int kOffV = kOffK + kNS * kTile;
+  static constexpr int kSmem = kOffV + kNS * kTile;
+};
 constexpr float kRescaleThr = 8.f;
 
 // structure flags (FA_FWD_VARIANT=22xx selects them for A/B timing)
@@ -60,12 +63,17 @@ constexpr int kFSumsLate = 4;  // row sums of P(i-1) in MFMA(i) instead of VALU(
 constexpr int kANoExp = 8, kANoMax = 16, kANoSums = 32;
 // ... and in the MFMA phase: no staging loads, no LDS stores, no fragment reads
 constexpr int kANoLoad = 64, kANoStore = 128, kANoFrag = 256;
+// staging by LDS-DMA (buffer_load ... lds straight into the ring, no VGPR round trip / ds_write)
+constexpr int kFDma = 512;
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
   constexpr float kNegInf = -__builtin_huge_valf();
+  constexpr bool DMA = (F & kFDma) != 0;
+  constexpr int kNS = Ring<DMA>::kNS;
+  constexpr int kOffV = Ring<DMA>::kOffV;
 
   const int nq = a.rule.q.n, nk = a.rule.k.n;
   const uint32_t nqb = (nq + kBM - 1) / kBM;
@@ -104,10 +112,34 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     return __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off : 0x80000000u, 2 * min(k0, nk), 0);
   };
   auto store = [&](int off, u32x4 v) __attribute__((always_inline)) { *reinterpret_cast<lds_u32x4_t*>(smem + off) = v; };
+  // LDS-DMA: wave w fills bytes [1024w, 1024w + 1024) of a tile image, lane L the 16 B at 16L:
+  // row c = 8w + L/8, position L%8, i.e. source chunk cm = pos ^ swizzle(c) (the images' XORs)
+  const int dpos = lane & 7, drow = 8 * w + (lane >> 3);
+  const int kcm = dpos ^ (4 * ((drow >> 1) & 1)), vcm = dpos ^ ((drow >> 1) & 7);
+  const uint32_t kdoff = drow < d ? (uint32_t)drow * (uint32_t)nk * 2u + 16u * kcm : 0x80000000u;
+  const uint32_t vdoff = drow < vd ? (uint32_t)drow * (uint32_t)nk * 2u + 16u * vcm : 0x80000000u;
+  auto dma = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, int cmx, int k0, int lds_off) __attribute__((always_inline)) {
+    const bool in = k0 + 8 * cmx < nk;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + lds_off + 1024 * w), 16,
+                                             in ? off : 0x80000000u, 2 * min(k0, nk), 0, 0);
+  };
 
+  u32x4 kst[3], vst[3];
+  if constexpr (DMA) {
+    // ---- prologue: K(0..4), V(0..3) by LDS-DMA, Q through registers
+#pragma unroll
+    for (int j = 0; j < kNS; ++j) dma(krs, kdoff, kcm, kt0 + j * kBN, kOffK + j * kTile);
+#pragma unroll
+    for (int j = 0; j < kNS - 1; ++j) dma(vrs, vdoff, vcm, kt0 + j * kBN, kOffV + j * kTile);
+    for (int idx = tid; idx < kD * (kBM / 8); idx += kNW * 64) {  // Q [64][256], 64-B blocks XOR-swizzled by c&3
+      const int c = idx / (kBM / 8), m = idx % (kBM / 8);
+      const u32x4 v = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec) : u32x4{0, 0, 0, 0};
+      *reinterpret_cast<lds_u32x4_t*>(smem + c * kQRow + ((m * 16) ^ ((c & 3) << 6))) = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): the DMA'd tiles have landed
+  } else {
   // ---- prologue: Q, K(0..2), V(0..1) into LDS; K(3..5), V(2..4) into the staging registers
   // (set j serves MFMA(i) with i mod 3 == j; loads run three steps ahead of their store)
-  u32x4 kst[kNS], vst[kNS];
   {
     u32x4 kp[3], vp[2];
 #pragma unroll
@@ -128,6 +160,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
       kst[j] = load(krs, koff, kt0 + (3 + j) * kBN);
       vst[j] = load(vrs, voff, kt0 + (2 + j) * kBN);
     }
+  }
   }
   __syncthreads();
 
@@ -297,13 +330,19 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     constexpr int c = decltype(C_)::value;  // it mod 3
     if (F & kFPrio) __builtin_amdgcn_s_setprio(1);
     // (unconditional: past the end these move zeros into slots nobody reads unmasked)
-    if (!(F & kANoStore)) {
-      store(kOffK + c * kTile + kwo, kst[c]);
-      store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
-    }
-    if (!(F & kANoLoad)) {
-      kst[c] = load(krs, koff, kt0 + (it + 6) * kBN);
-      vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
+    if constexpr (DMA) {
+      // K(i+5) over K(i) (its fragments were read in MFMA(i-1)), V(i+4) over V(i-1)
+      dma(krs, kdoff, kcm, kt0 + (it + kNS) * kBN, kOffK + c * kTile);
+      dma(vrs, vdoff, vcm, kt0 + (it + kNS - 1) * kBN, kOffV + ((c + kNS - 1) % kNS) * kTile);
+    } else {
+      if (!(F & kANoStore)) {
+        store(kOffK + c * kTile + kwo, kst[c]);
+        store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
+      }
+      if (!(F & kANoLoad)) {
+        kst[c] = load(krs, koff, kt0 + (it + 6) * kBN);
+        vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
+      }
     }
     if (tcls(it) != 0) {
 #pragma unroll
@@ -323,6 +362,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
       }
     }
     if (!(F & kANoFrag)) read_v(c);
+    // DMA: the tiles issued three MFMA phases ago (K(i+2), V(i+1), read from MFMA(i+1) on) have
+    // landed before this wave's next barrier: all but its six most recent DMAs are done
+    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(0x0F76);  // vmcnt(6)
     // No lgkmcnt drain here: a wave's LDS operations complete in order, and each wave waits for
     // its fragment reads before the MFMAs that use them (MFMA(i+1)), which orders its stores of
     // this phase before any other wave reads those tiles (MFMA(i+2)) and its reads before any
@@ -353,6 +395,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   // enters it one barrier late and group 0 leaves it one barrier late, so every barrier
   // interval pairs one group's MFMA(i) with the other's VALU phase.
   read_k(0);
+  if constexpr (DMA) __builtin_amdgcn_s_waitcnt(0xC07F);  // K(0)'s slot is DMA'd over in MFMA(0)
   if (grp == 1) __builtin_amdgcn_s_barrier();
   auto iter = [&](auto C_, int it) __attribute__((always_inline)) {
     stamp(-1);
@@ -371,6 +414,10 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     iter(IC<0>{}, it);
     iter(IC<1>{}, it + 1);
     iter(IC<2>{}, it + 2);
+    if constexpr (kNS > 3) {
+      iter(IC<3 % kNS>{}, it + 3);
+      iter(IC<4 % kNS>{}, it + 4);
+    }
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();
 
@@ -414,10 +461,11 @@ template <int F>
 hipError_t launch_t(const FwdArgs& a, hipStream_t s) {
   const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
   auto kern = a.rule.policy == 0 ? fwd_f16_pingpong_kernel<0, F> : fwd_f16_pingpong_kernel<1, F>;
+  constexpr int smem = Ring<(F & kFDma) != 0>::kSmem;
   hipError_t e =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kNW * 64), kSmem, s, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kNW * 64), smem, s, a);
   return hipGetLastError();
 }
 
@@ -436,6 +484,7 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
   switch (ev ? atoi(ev) : -1) {
     case 2200: return launch_t<0>(a, s);
     case 2203: return launch_t<kFPrio | kFStamp>(a, s);
+    case 2212: return launch_t<kFPrio | kFDma>(a, s);
     case 2205: return launch_t<kFPrio | kFSumsLate>(a, s);
     case 2211: return launch_t<kFPrio | kFStamp | kANoExp>(a, s);
     case 2219: return launch_t<kFPrio | kFStamp | kANoMax>(a, s);
