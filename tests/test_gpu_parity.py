@@ -330,3 +330,35 @@ def test_config4_local_window256_sampled():
 def test_config5_full2d_f32_sampled():
     """Config 5 shape at reduced batch: full_2d fp32 (64,64) vs (128,128), scale_front."""
     run_case(np.float32, "full", 2, "scale_front", (1, 2), 64, 64, (64, 64), (128, 128), seed=5, slices=[1])
+
+
+# ------------------------------ alternative fp16 kernel structures (selected per call by env)
+# FA_FWD_VARIANT / FA_BWD_VARIANT pick the opt-in structures the dispatcher does not choose by
+# default (DESIGN.md §3.0, §3.2); each must stay parity-green on every rule it accepts:
+#   2000 paired-block forward, 2200 ping-pong forward without priority flips, 2201 ping-pong
+#   forward (the full-policy default, forced here for causal / local too), 2212 ping-pong with
+#   LDS-DMA staging, 1814 the 8-wave forward that the ping-pong kernel replaced, and
+#   bwd 1281 the software-pipelined dK/dV pass (d = 128).
+VARIANT_CASES = [
+    ("full", 1, "none_front", (264,), (136,), 1, False, 64, 64),
+    ("full", 1, "none_front", (300,), (1000,), 1, False, 48, 64),
+    ("causal", 1, "none_front", (392,), (392,), 1, False, 64, 64),
+    ("causal", 1, "scale_end", (200,), (520,), 1, False, 64, 40),
+    ("local", 1, "none_front", (700,), (700,), 33, False, 64, 64),
+    ("local", 1, "scale_front", (240,), (480,), 70, True, 64, 64),
+    ("causal", 2, "scale_front", (8, 24), (16, 16), 1, False, 64, 64),
+]
+
+
+@pytest.mark.parametrize("variant", ["2000", "2200", "2201", "2212", "1814"])
+@pytest.mark.parametrize("policy,seq_dims,mode,qs,ks,ws,causal,d,vd", VARIANT_CASES)
+def test_f16_forward_structures(monkeypatch, variant, policy, seq_dims, mode, qs, ks, ws, causal, d, vd):
+    monkeypatch.setenv("FA_FWD_VARIANT", variant)
+    run_case(np.float16, policy, seq_dims, mode, (2, 2), d, vd, qs, ks, ws=ws, ls=0, causal=causal, bwd=False,
+             seed=int(variant) + d + ws)
+
+
+@pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, False)])
+def test_f16_backward_pipelined_dkdv(monkeypatch, policy, ws, causal):
+    monkeypatch.setenv("FA_BWD_VARIANT", "1281")
+    run_case(np.float16, policy, 1, "none_front", (2,), 128, 128, (328,), (264,), ws=ws, ls=0, causal=causal, seed=7)
