@@ -78,6 +78,13 @@ constexpr int kGPad = 1;  // G image rows of padding (16 B) per group
 __device__ __forceinline__ uint32_t qt_off(int row, int col) {  // col multiple of 4
   return row * 64 + ((((col >> 2) ^ (row >> 2)) & 7) << 3);
 }
+// "Q16 image" [D][32] fp16, 64-B rows, 16-B units XOR-swizzled by (row >> 2) & 3: one ds_write_b128
+// per staged chunk; conflict-free transposed reads (rows q = 0..3 of a 4-row block fill the four
+// 64-B quarters of the bank window) and conflict-free b128 row reads (16 lanes = 16 rows).
+// Byte offset of the 8-B half `half8` of unit u (8 queries 8u..8u+7) of row `row`.
+__device__ __forceinline__ uint32_t q16_off(int row, int u, int half8 = 0) {
+  return row * 64 + 16 * (u ^ ((row >> 2) & 3)) + 8 * half8;
+}
 __device__ __forceinline__ uint32_t kt_off(int row, int col) {  // col multiple of 4 (or 8)
   return row * 128 + ((col * 2) ^ ((row & 2) << 5));
 }
@@ -99,7 +106,7 @@ struct DkdvSmem {
   static constexpr int kRow = D * kBK * 2;            // K (or V) row image
   static constexpr int kQT = D * 64;                  // one [D][32] QT image
   static constexpr int kG = 4 * (D + kGPad) * 16;     // one 32-column G image
-  static constexpr int offQT = 0, offOT = kQT, offQG = 2 * kQT, offOG = 2 * kQT + kG, offLse = 2 * kQT + 2 * kG;
+  static constexpr int offQT = 0, offOT = kQT, offLse = 2 * kQT;
   static constexpr int kSlot = offLse + 2 * 32 * 4;   // + lse2[32], D[32]
   static constexpr int kRing = NS * kSlot;
   static constexpr int kTotal = (kRing > 2 * kRow) ? kRing : 2 * kRow;  // the K/V images alias the ring
@@ -112,7 +119,9 @@ struct DkdvSmem {
 // the dV / dK MFMAs of tile it; the LDS latency of one tile's operand reads and the VALU
 // work hide under the other tile's MFMAs (a single wave per SIMD has nothing else to hide
 // them behind).  One workgroup = NW waves x 32 keys of one (batch, head) slice.
-template <int D, int NW, int WPE, int POL, bool PIPE = false>
+// ablation bits (timing diagnostics, outputs WRONG; FA_BWD_VARIANT=1300+bits, d = 128):
+// 1 no exp2, 2 no tile stores, 4 no tile loads, 8 no Q/dO transposed reads, 16 no G-image reads, 32 no barrier
+template <int D, int NW, int WPE, int POL, bool PIPE = false, int ABL = 0>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -132,6 +141,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, r = lane & 31;
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  // transposed reads of the Q16 images supply query columns 4σ(p)..4σ(p)+3 (σ swaps 1 and 2), so
+  // register i of S / dP holds query 16(i>>3) + 8h + (i&7): k-step s of P / dS is queries
+  // 16s + 8h + 0..7, and the dV / dK A operands are plain 16-B row reads of the same images
+  const int sig = ((tp & 1) << 1) | (tp >> 1);
   const float c2 = (float)a.scale * kLog2e;
 
   // channels d (Q/K) and v_d (V/O) may be smaller than D: rows past them are staged as zeros
@@ -209,36 +222,34 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
     cm_[j] = idx & 3;
     voff[j] = (uint32_t)crow_[j] * (uint32_t)nq * 2u + 16u * cm_[j];
   }
-  u32x4 qr[kCPT];
-  float lr = 0.f;
+  // two staging sets (tile t in set t&1): a tile is loaded two steps before it is stored
+  u32x4 qr[2][kCPT];
+  float lr[2] = {0.f, 0.f};
   // chunk j holds dO (else Q); compile-time when the chunks divide evenly over the threads
   auto is_o = [&](int j) -> bool {
     return (kQChunks % kThr == 0) ? (j >= kQChunks / kThr) : ((tid + kThr * j) >= kQChunks);
   };
-  auto load_tile = [&](int qa) {
+  auto load_tile = [&](int qa, int set) {
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) {
       const bool isO = is_o(j);
       const bool out = qa + 8 * cm_[j] >= nq || crow_[j] >= (isO ? vd : d);
-      qr[j] = buf_load16(isO ? ors : qrs, voff[j], 2 * qa, out);
+      qr[set][j] = buf_load16(isO ? ors : qrs, voff[j], 2 * qa, out);
     }
     if (tid < 64) {  // lanes 0..31: lse2, 32..63: D
       const int q = qa + (tid & 31);
-      lr = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? __builtin_huge_valf() : 0.f);
+      lr[set] = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? __builtin_huge_valf() : 0.f);
     }
   };
-  auto store_tile = [&](int slot) {
+  auto store_tile = [&](int slot, int set) {
     lds_char_t* base = smem + slot * S::kSlot;
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) {
       const bool isO = is_o(j);
       lds_char_t* t = base + (isO ? S::offOT : S::offQT);
-      lds_char_t* gi = base + (isO ? S::offOG : S::offQG);
-      *reinterpret_cast<lds_u32x2_t*>(t + qt_off(crow_[j], 8 * cm_[j])) = qr[j].xy;
-      *reinterpret_cast<lds_u32x2_t*>(t + qt_off(crow_[j], 8 * cm_[j] + 4)) = qr[j].zw;
-      g_store<D>(gi, crow_[j], cm_[j], qr[j]);
+      *reinterpret_cast<lds_u32x4_t*>(t + q16_off(crow_[j], cm_[j])) = qr[set][j];
     }
-    if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr;
+    if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr[set];
   };
 
   floatx16 dk[D / 32], dv[D / 32];
@@ -250,9 +261,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   // row constants of the tile in `base` as initial accumulators: S: -lse2[q], dP: -D[q]
   auto init_acc = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) {
 #pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      const floatx4 l4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 4 * (8 * gq + 4 * h));
-      const floatx4 d4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 128 + 4 * (8 * gq + 4 * h));
+    for (int gq = 0; gq < 4; ++gq) {  // registers 4gq..4gq+3 = queries 16(gq>>1) + 8h + 4(gq&1) + 0..3
+      const int q4 = 16 * (gq >> 1) + 8 * h + 4 * (gq & 1);
+      const floatx4 l4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 4 * q4);
+      const floatx4 d4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 128 + 4 * q4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         sacc[4 * gq + j] = -l4[j];
@@ -265,11 +277,16 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
       half8 qa8, oa8;
+      if (ABL & 8) {
+        qa8 = kb[(s + 1) % (D / 16)];
+        oa8 = vb[(s + 1) % (D / 16)];
+      } else {
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const uint32_t off = qt_off(16 * s + 8 * (g >> 1) + 4 * e + tq, 16 * (g & 1) + 4 * tp);
-        const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
-        if (e == 0) { qa8.lo = x; oa8.lo = y; } else { qa8.hi = x; oa8.hi = y; }
+        for (int e = 0; e < 2; ++e) {
+          const uint32_t off = q16_off(16 * s + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
+          const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
+          if (e == 0) { qa8.lo = x; oa8.lo = y; } else { qa8.hi = x; oa8.hi = y; }
+        }
       }
       sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8, kb[s], sacc, 0, 0, 0);
       pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8, vb[s], pacc, 0, 0, 0);
@@ -279,9 +296,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   auto softmax = [&](const floatx16& sacc, const floatx16& pacc, int qa, int cls, half8 (&pf)[2], half8 (&sf)[2]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float pv = __builtin_amdgcn_exp2f(sacc[i]);
+      float pv = (ABL & 1) ? sacc[i] : __builtin_amdgcn_exp2f(sacc[i]);
       if (POL == 1 && cls == 1) {
-        const int q = qa + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
         pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
       }
       pf[i >> 3][i & 7] = (_Float16)pv;
@@ -294,25 +311,29 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int u = 0; u < D / 32; ++u) {
-        const half8 oa = read_b128(base + S::offOG + g_off<D>(s, h, 32 * u + r));
-        const half8 qa = read_b128(base + S::offQG + g_off<D>(s, h, 32 * u + r));
+        const half8 oa = (ABL & 16) ? vb[2 * s + u] : read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s + h));
+        const half8 qa = (ABL & 16) ? kb[2 * s + u] : read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s + h));
         dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa, pf[s], dv[u], 0, 0, 0);
         dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa, sf[s], dk[u], 0, 0, 0);
       }
   };
 
   if constexpr (!PIPE) {
-    if (ntiles > 0) { load_tile(qt0); store_tile(0); }
-    if (ntiles > 1) load_tile(qt0 + 32);
+    if (ntiles > 0) { load_tile(qt0, 0); store_tile(0, 0); }
+    load_tile(qt0 + 32, 1);
+    load_tile(qt0 + 64, 0);
 
     // iteration it: tile it in slot it&1 (complete after the barrier); tile it+1 -> slot (it+1)&1
-    // (read in iteration it-1, finished before this barrier); tile it+2 -> registers
+    // (read in iteration it-1, finished before this barrier) from staging set (it+1)&1, which then
+    // takes tile it+3.  Loads and stores are unconditional (past the end they move zeros into
+    // a slot nobody reads), so hipcc's vmcnt waits stay exact: a store waits only for the load
+    // issued two steps earlier.
     auto step = [&](auto P_, int it) {
       constexpr int p = decltype(P_)::value;
-      __syncthreads();
+      if (!(ABL & 32)) __syncthreads();
       const int qa = qt0 + 32 * it;
-      if (it + 1 < ntiles) store_tile(p ^ 1);
-      if (it + 2 < ntiles) load_tile(qa + 64);
+      if (!(ABL & 2)) store_tile(p ^ 1, p ^ 1);
+      if (!(ABL & 4)) load_tile(qa + 96, p ^ 1);
       const int cls = tcls(qa);
       if (cls == 0) return;
       const lds_char_t* base = smem + p * S::kSlot;
@@ -331,9 +352,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
     // tile j lives in slot j % 3; step it: barrier (tile it+1 complete), tile it+2 -> slot
     // (it+2)%3 (tile it-1's, finished in step it-1), tile it+3 -> registers; S/dP(it+1) beside
     // the softmax of tile it; dV/dK(it)
-    if (ntiles > 0) { load_tile(qt0); store_tile(0); }
-    if (ntiles > 1) { load_tile(qt0 + 32); store_tile(1); }
-    if (ntiles > 2) load_tile(qt0 + 64);
+    if (ntiles > 0) { load_tile(qt0, 0); store_tile(0, 0); }
+    if (ntiles > 1) { load_tile(qt0 + 32, 0); store_tile(1, 0); }
+    if (ntiles > 2) load_tile(qt0 + 64, 0);
     __syncthreads();
     floatx16 sa, pa, sb, pb;  // S / dP accumulators of two consecutive tiles
     if (ntiles > 0 && tcls(qt0) != 0) {
@@ -344,8 +365,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       constexpr int c = decltype(C_)::value;  // it mod 3
       __syncthreads();
       const int qa = qt0 + 32 * it;
-      if (it + 2 < ntiles) store_tile((c + 2) % 3);
-      if (it + 3 < ntiles) load_tile(qa + 96);
+      if (it + 2 < ntiles) store_tile((c + 2) % 3, 0);
+      if (it + 3 < ntiles) load_tile(qa + 96, 0);
       const int cls = tcls(qa);
       const int cls1 = (it + 1 < ntiles) ? tcls(qa + 32) : 0;
       const lds_char_t* base = smem + c * S::kSlot;
@@ -604,11 +625,11 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     }
 }
 
-template <int D, int NW, int WPE, bool PIPE = false>
+template <int D, int NW, int WPE, bool PIPE = false, int ABL = 0>
 hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
   using S = DkdvSmem<D, NW, PIPE ? 3 : 2>;
   const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
-  auto kern = a.rule.policy == 0 ? bwd_dkdv_kernel<D, NW, WPE, 0, PIPE> : bwd_dkdv_kernel<D, NW, WPE, 1, PIPE>;
+  auto kern = a.rule.policy == 0 ? bwd_dkdv_kernel<D, NW, WPE, 0, PIPE, ABL> : bwd_dkdv_kernel<D, NW, WPE, 1, PIPE, ABL>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      S::kTotal);
   if (e != hipSuccess) return e;
@@ -662,7 +683,18 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
       default: return launch_dq<64, 4, 2>(a, s);
     }
   }
-  e = (v == 1281) ? launch_dkdv<128, 4, 1, true>(a, s) : launch_dkdv<128, 4, 1>(a, s);
+  switch (v) {
+    case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
+    case 1301: e = launch_dkdv<128, 4, 1, false, 1>(a, s); break;
+    case 1302: e = launch_dkdv<128, 4, 1, false, 2>(a, s); break;
+    case 1304: e = launch_dkdv<128, 4, 1, false, 4>(a, s); break;
+    case 1308: e = launch_dkdv<128, 4, 1, false, 8>(a, s); break;
+    case 1316: e = launch_dkdv<128, 4, 1, false, 16>(a, s); break;
+    case 1324: e = launch_dkdv<128, 4, 1, false, 24>(a, s); break;
+    case 1338: e = launch_dkdv<128, 4, 1, false, 38>(a, s); break;
+    case 1363: e = launch_dkdv<128, 4, 1, false, 63>(a, s); break;
+    default: e = launch_dkdv<128, 4, 1>(a, s); break;
+  }
   if (e != hipSuccess) return e;
   return launch_dq<128, 4, 1>(a, s);
 }
