@@ -65,19 +65,6 @@ __global__ __launch_bounds__(kThrPrep) void bwd_prep_kernel(BwdArgs a) {
 // LDS images
 //   "row image"  [D][W] fp16, W = 32*NW columns, 16-B chunks XOR-swizzled by (row & 3) << 6
 //                (B-operand transposed reads conflict-free; the forward's Q tile)
-//   "KT image"   [D][64] fp16, 128-B rows, 64-B halves swapped on rows with c&2
-//                (A operand Kᵀ / Vᵀ of a 64-key tile by transposed reads)
-//   "G image"    [2*nb groups][D+1][8] fp16: group (s, h) holds columns
-//                {16s + 4h + 0..3, 16s + 8 + 4h + 0..3} of each row, so one ds_read_b128
-//                is the A operand whose k order matches a 32x32 accumulator's register
-//                order (P / dS used as B operands without any shuffle)
-//   "QT image"   [D][32] fp16, 64-B rows, 8-B chunks XOR-swizzled by row>>2
-//                (A operand Qᵀ / dOᵀ of a 32-query tile by transposed reads)
-constexpr int kGPad = 1;  // G image rows of padding (16 B) per group
-
-__device__ __forceinline__ uint32_t qt_off(int row, int col) {  // col multiple of 4
-  return row * 64 + ((((col >> 2) ^ (row >> 2)) & 7) << 3);
-}
 // "Q16 image" [D][32] fp16, 64-B rows, 16-B units XOR-swizzled by (row >> 2) & 3: one ds_write_b128
 // per staged chunk; conflict-free transposed reads (rows q = 0..3 of a 4-row block fill the four
 // 64-B quarters of the bank window) and conflict-free b128 row reads (16 lanes = 16 rows).
@@ -85,27 +72,18 @@ __device__ __forceinline__ uint32_t qt_off(int row, int col) {  // col multiple 
 __device__ __forceinline__ uint32_t q16_off(int row, int u, int half8 = 0) {
   return row * 64 + 16 * (u ^ ((row >> 2) & 3)) + 8 * half8;
 }
-__device__ __forceinline__ uint32_t kt_off(int row, int col) {  // col multiple of 4 (or 8)
-  return row * 128 + ((col * 2) ^ ((row & 2) << 5));
+// "K2 image" [D][64] fp16, 128-B rows, 16-B chunk j at position j ^ (4·bit1(row) + bits2..3(row)):
+// conflict-free for the σ-permuted transposed reads (a 4-row block's rows 0/2 and 1/3 land in
+// opposite 64-B halves) AND for b128 row reads (16 consecutive rows hit 16 distinct 16-B slots),
+// so one image serves as Kᵀ (Sᵀ = Kᵀ·Q') and as K (dQ += K·dSᵀ).
+__device__ __forceinline__ uint32_t k2_off(int row, int j, int half8 = 0) {
+  return row * 128 + 16 * (j ^ (4 * ((row >> 1) & 1) + ((row >> 2) & 3))) + 8 * half8;
 }
-template <int D>
-__device__ __forceinline__ uint32_t g_off(int s, int h, int row) {
-  return ((2 * s + h) * (D + kGPad) + row) * 16;
-}
-// chunk m (8 consecutive columns 8m..8m+7) of row c -> two 8-B halves of the G image
-template <int D>
-__device__ __forceinline__ void g_store(lds_char_t* img, int c, int m, u32x4 v) {
-  lds_char_t* p = img + g_off<D>(m >> 1, 0, c) + (m & 1) * 8;
-  *reinterpret_cast<lds_u32x2_t*>(p) = v.xy;
-  *reinterpret_cast<lds_u32x2_t*>(p + (D + kGPad) * 16) = v.zw;
-}
-
 template <int D, int NW, int NS = 2>
 struct DkdvSmem {
   static constexpr int kBK = 32 * NW;                 // keys per workgroup
   static constexpr int kRow = D * kBK * 2;            // K (or V) row image
   static constexpr int kQT = D * 64;                  // one [D][32] QT image
-  static constexpr int kG = 4 * (D + kGPad) * 16;     // one 32-column G image
   static constexpr int offQT = 0, offOT = kQT, offLse = 2 * kQT;
   static constexpr int kSlot = offLse + 2 * 32 * 4;   // + lse2[32], D[32]
   static constexpr int kRing = NS * kSlot;
@@ -305,7 +283,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       sf[i >> 3][i & 7] = (_Float16)(pv * pacc[i]);
     }
   };
-  // dV += dO·P, dK += Q·dS: A = X[row 32u + r][group (s, h)] (G images)
+  // dV += dO·P, dK += Q·dS: A = X[row 32u + r][queries 16s + 8h + 0..7] (b128 reads of the Q16 images)
   auto dvdk = [&](const lds_char_t* base, const half8 (&pf)[2], const half8 (&sf)[2]) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -416,9 +394,8 @@ struct DqSmem {
   static constexpr int kBM = 32 * NW;                 // queries per workgroup
   static constexpr int kRow = D * kBM * 2;            // Q (or dO) row image
   static constexpr int kKT = D * 128;                 // one [D][64] KT image
-  static constexpr int kG = 8 * (D + kGPad) * 16;     // one 64-column G image
-  static constexpr int offKT = 0, offVT = kKT, offKG = 2 * kKT;
-  static constexpr int kSlot = 2 * kKT + kG;
+  static constexpr int offKT = 0, offVT = kKT;
+  static constexpr int kSlot = 2 * kKT;
   static constexpr int kRing = 2 * kSlot;
   static constexpr int kTotal = (kRing > 2 * kRow) ? kRing : 2 * kRow;  // the Q/dO images alias the ring
 };
@@ -545,8 +522,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) {
       const bool isV = is_v(j);
-      *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + kt_off(crow_[j], 8 * cm)) = kr[j];
-      if (!isV) g_store<D>(base + S::offKG, crow_[j], cm, kr[j]);
+      *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[j];
     }
   };
 
@@ -556,9 +532,18 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[u][i] = 0.f;
 
-  // A-operand (Kᵀ / Vᵀ) read bases: element (crow, col) of a KT image
-  const uint32_t tb0 = kt_off(8 * (g >> 1) + tq, 16 * (g & 1) + 4 * tp);
-  const uint32_t tb1 = kt_off(8 * (g >> 1) + tq, 32 + 16 * (g & 1) + 4 * tp);
+  // A-operand (Kᵀ / Vᵀ) read bases: lane 4q+p of a 16-lane group supplies channel row q, keys
+  // 4σ(p)..4σ(p)+3 (σ swaps 1 and 2), so register i of Sᵀ / dPᵀ half t holds key 32t + 16(i>>3) +
+  // 8h + (i&7): k-step s of dSᵀ is keys 16s + 8h + 0..7 and K's dQ A operand is one b128 row read
+  const int sig = ((tp & 1) << 1) | (tp >> 1);
+  uint32_t tb[2][2];  // [e][t], row 8(g>>1) + 4e + tq (+16s: immediate)
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) tb[e][t] = k2_off(8 * (g >> 1) + 4 * e + tq, 4 * t + 2 * (g & 1) + (sig >> 1), sig & 1);
+  uint32_t kb2[4];  // dQ A operand: row 32u + r (+32u·128: immediate), chunk 2s + h
+#pragma unroll
+  for (int s = 0; s < 4; ++s) kb2[s] = k2_off(r, 2 * s + h);
 
   if (ntiles > 0) { load_tile(kt0); store_tile(0); }
   if (ntiles > 1) load_tile(kt0 + kBN);
@@ -578,15 +563,15 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         half8 kf, vf;
-        const uint32_t b = (t ? tb1 : tb0) + (16 * s) * 128;
-        kf.lo = tr_read(base + S::offKT + b);
-        kf.hi = tr_read(base + S::offKT + b + 4 * 128);
-        vf.lo = tr_read(base + S::offVT + b);
-        vf.hi = tr_read(base + S::offVT + b + 4 * 128);
+        const uint32_t b0 = tb[0][t] + (16 * s) * 128, b1 = tb[1][t] + (16 * s) * 128;
+        kf.lo = tr_read(base + S::offKT + b0);
+        kf.hi = tr_read(base + S::offKT + b1);
+        vf.lo = tr_read(base + S::offVT + b0);
+        vf.hi = tr_read(base + S::offVT + b1);
         st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], s == 0 ? negl : st[t], 0, 0, 0);
         dp[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, of[s], s == 0 ? negd : dp[t], 0, 0, 0);
       }
-    // dSᵀ = exp2(Sᵀ)∘dPᵀ; keys of register i of half t: 32t + (i&3) + 8(i>>2) + 4h
+    // dSᵀ = exp2(Sᵀ)∘dPᵀ; keys of register i of half t: 32t + 16(i>>3) + 8h + (i&7)
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       half8 dsf;
@@ -595,7 +580,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
         const int t = s >> 1, i = 8 * (s & 1) + j;
         float pv = __builtin_amdgcn_exp2f(st[t][i]);
         if (cls == 1) {
-          const int kk = ka + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+          const int kk = ka + 32 * t + 16 * (i >> 3) + 8 * h + (i & 7);
           const bool ok = (POL == 1) ? ((unsigned)(kk - klo) < (unsigned)kspan) : (kk < nk);
           pv = ok ? pv : 0.f;
         }
@@ -603,7 +588,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < D / 32; ++u) {
-        const half8 ka8 = read_b128(base + S::offKG + g_off<D>(s, h, 32 * u + r));
+        const half8 ka8 = read_b128(base + S::offKT + kb2[s] + 32 * u * 128);
         dq[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka8, dsf, dq[u], 0, 0, 0);
       }
     }
