@@ -505,24 +505,25 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     crow_[j] = ((tid + kThr * j) % kKChunks) >> 3;
     voff[j] = (uint32_t)crow_[j] * (uint32_t)nk * 2u + 16u * cm;
   }
-  u32x4 kr[kCPT];
+  // two staging sets (tile t in set t&1): a tile is loaded two steps before it is stored
+  u32x4 kr[2][kCPT];
   auto is_v = [&](int j) -> bool {
     return (kKChunks % kThr == 0) ? (j >= kKChunks / kThr) : ((tid + kThr * j) >= kKChunks);
   };
-  auto load_tile = [&](int ka) {
+  auto load_tile = [&](int ka, int set) {
     const bool out = ka + 8 * cm >= nk;
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) {
       const bool isV = is_v(j);
-      kr[j] = buf_load16(isV ? vrs : krs, voff[j], 2 * ka, out || crow_[j] >= (isV ? vd : d));
+      kr[set][j] = buf_load16(isV ? vrs : krs, voff[j], 2 * min(ka, nk), out || crow_[j] >= (isV ? vd : d));
     }
   };
-  auto store_tile = [&](int slot) {
+  auto store_tile = [&](int slot, int set) {
     lds_char_t* base = smem + slot * S::kSlot;
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) {
       const bool isV = is_v(j);
-      *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[j];
+      *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[set][j];
     }
   };
 
@@ -545,15 +546,17 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) kb2[s] = k2_off(r, 2 * s + h);
 
-  if (ntiles > 0) { load_tile(kt0); store_tile(0); }
-  if (ntiles > 1) load_tile(kt0 + kBN);
+  if (ntiles > 0) { load_tile(kt0, 0); store_tile(0, 0); }
+  load_tile(kt0 + kBN, 1);
+  load_tile(kt0 + 2 * kBN, 0);
 
   auto step = [&](auto P_, int it) {
     constexpr int p = decltype(P_)::value;
     __syncthreads();
     const int ka = kt0 + it * kBN;
-    if (it + 1 < ntiles) store_tile(p ^ 1);
-    if (it + 2 < ntiles) load_tile(ka + 2 * kBN);
+    // unconditional (past the end they move zeros into a slot nobody reads): exact vmcnt waits
+    store_tile(p ^ 1, p ^ 1);
+    load_tile(ka + 3 * kBN, p ^ 1);
     const int cls = tcls(ka);
     if (cls == 0) return;
     const lds_char_t* base = smem + p * S::kSlot;
