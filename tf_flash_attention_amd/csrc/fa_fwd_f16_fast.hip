@@ -490,6 +490,11 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
   // FA_FWD_VARIANT=22xx forces it (and its variants) for every rule it takes
   if (fwd_f16_pingpong_supported(a) && ((v < 0 && a.rule.policy == 0) || (v >= 2200 && v < 2300)))
     return launch_fwd_f16_pingpong(a, s);
+  // d in (64, 128]: the ping-pong kernel is the default for the full and causal policies (c3
+  // forward: 2.52 vs 3.16 ms for the 4-wave kernel below); local windows keep the 4-wave blocks
+  // (short rule-bounded rows); FA_FWD_VARIANT=23xx forces it for every rule it takes
+  if (fwd_f16_pingpong128_supported(a) && ((v < 0 && a.rule.policy != 2) || (v >= 2300 && v < 2400)))
+    return launch_fwd_f16_pingpong128(a, s);
   if (d64 && v == 1899) {  // ablations (timing only)
     const char* e = getenv("FA_FWD_ABL");
     switch (e ? atoi(e) : 0) {

@@ -61,6 +61,9 @@ hipError_t launch_fwd_f16_pp(const FwdArgs& a, hipStream_t s);
 // ping-pong fp16 forward (8 waves, two groups alternating MFMA / softmax phases) — fa_fwd_f16_pingpong.hip
 bool fwd_f16_pingpong_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s);
+// ping-pong fp16 forward for 64 < max(d, v_d) <= 128 — fa_fwd_f16_pingpong128.hip
+bool fwd_f16_pingpong128_supported(const FwdArgs& a);
+hipError_t launch_fwd_f16_pingpong128(const FwdArgs& a, hipStream_t s);
 bool bwd_f16_supported(const BwdArgs& a);
 // fp32 MFMA forward — fa_fwd_f32.hip
 bool fwd_f32_supported(const FwdArgs& a);
