@@ -65,6 +65,12 @@ constexpr int kANoExp = 8, kANoMax = 16, kANoSums = 32;
 constexpr int kANoLoad = 64, kANoStore = 128, kANoFrag = 256;
 // staging by LDS-DMA (buffer_load ... lds straight into the ring, no VGPR round trip / ds_write)
 constexpr int kFDma = 512;
+// diagnostic: workgroup timeline (s_memrealtime at entry / after the prologue / after the loop /
+// at exit, cycle counts, HW_ID, XCC_ID) written as raw words over the block's first l entries
+constexpr int kFStampWG = 2048;
+// the MFMA phase's staging stores after its MFMAs and fragment reads (their vmcnt waits and
+// store-path cycles under the running PV MFMAs); lgkmcnt(0) at the start of the VALU phase
+constexpr int kFStoresLate = 4096;
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
@@ -75,6 +81,11 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   constexpr int kNS = Ring<DMA>::kNS;
   constexpr int kOffV = Ring<DMA>::kOffV;
 
+  uint64_t wg_t0 = 0, wg_c0 = 0;
+  if constexpr ((F & kFStampWG) != 0) {
+    wg_t0 = __builtin_amdgcn_s_memrealtime();
+    wg_c0 = __builtin_amdgcn_s_memtime();
+  }
   const int nq = a.rule.q.n, nk = a.rule.k.n;
   const uint32_t nqb = (nq + kBM - 1) / kBM;
   const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -141,25 +152,47 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   // ---- prologue: Q, K(0..2), V(0..1) into LDS; K(3..5), V(2..4) into the staging registers
   // (set j serves MFMA(i) with i mod 3 == j; loads run three steps ahead of their store)
   {
+    // every load of the prologue in flight at once (the staging registers' too): one memory
+    // latency before the loop instead of two
     u32x4 kp[3], vp[2];
 #pragma unroll
     for (int j = 0; j < 3; ++j) kp[j] = load(krs, koff, kt0 + j * kBN);
 #pragma unroll
     for (int j = 0; j < 2; ++j) vp[j] = load(vrs, voff, kt0 + j * kBN);
-    for (int idx = tid; idx < kD * (kBM / 8); idx += kNW * 64) {  // Q [64][256], 64-B blocks XOR-swizzled by c&3
-      const int c = idx / (kBM / 8), m = idx % (kBM / 8);
-      const u32x4 v = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec) : u32x4{0, 0, 0, 0};
-      *reinterpret_cast<lds_u32x4_t*>(smem + c * kQRow + ((m * 16) ^ ((c & 3) << 6))) = v;
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) store(kOffK + j * kTile + kwo, kp[j]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) store(kOffV + j * kTile + vwo, vp[j]);
 #pragma unroll
     for (int j = 0; j < kNS; ++j) {
       kst[j] = load(krs, koff, kt0 + (3 + j) * kBN);
       vst[j] = load(vrs, voff, kt0 + (2 + j) * kBN);
     }
+    // Q [64][256], 64-B blocks XOR-swizzled by c&3: four chunks a thread, all loads before the stores
+    // (a rolled loop here serialised four memory latencies: ~6000 cycles of prologue)
+    constexpr int kQPT = kD * (kBM / 8) / (kNW * 64);
+    u32x4 qv[kQPT];
+    if (qvec) {  // branch-free buffer loads (chunks past d or nq read as zeros)
+      const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Q, 2u * d * nq);
+#pragma unroll
+      for (int j = 0; j < kQPT; ++j) {
+        const int idx = tid + j * kNW * 64, c = idx / (kBM / 8), m = idx % (kBM / 8);
+        const bool in = c < d && q0 + 8 * m < nq;
+        qv[j] = __builtin_amdgcn_raw_buffer_load_b128(qrs, in ? (uint32_t)c * (uint32_t)nq * 2u + 16u * m : 0x80000000u,
+                                                      2 * q0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kQPT; ++j) {
+        const int idx = tid + j * kNW * 64, c = idx / (kBM / 8), m = idx % (kBM / 8);
+        qv[j] = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, false) : u32x4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kQPT; ++j) {
+      const int idx = tid + j * kNW * 64, c = idx / (kBM / 8), m = idx % (kBM / 8);
+      *reinterpret_cast<lds_u32x4_t*>(smem + c * kQRow + ((m * 16) ^ ((c & 3) << 6))) = qv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) store(kOffK + j * kTile + kwo, kp[j]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) store(kOffV + j * kTile + vwo, vp[j]);
   }
   }
   __syncthreads();
@@ -335,11 +368,11 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
       dma(krs, kdoff, kcm, kt0 + (it + kNS) * kBN, kOffK + c * kTile);
       dma(vrs, vdoff, vcm, kt0 + (it + kNS - 1) * kBN, kOffV + ((c + kNS - 1) % kNS) * kTile);
     } else {
-      if (!(F & kANoStore)) {
+      if (!(F & (kANoStore | kFStoresLate))) {
         store(kOffK + c * kTile + kwo, kst[c]);
         store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
       }
-      if (!(F & kANoLoad)) {
+      if (!(F & (kANoLoad | kFStoresLate))) {
         kst[c] = load(krs, koff, kt0 + (it + 6) * kBN);
         vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
       }
@@ -362,6 +395,12 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
       }
     }
     if (!(F & kANoFrag)) read_v(c);
+    if constexpr ((F & kFStoresLate) != 0 && !DMA) {
+      store(kOffK + c * kTile + kwo, kst[c]);
+      store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
+      kst[c] = load(krs, koff, kt0 + (it + 6) * kBN);
+      vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
+    }
     // DMA: the tiles issued three MFMA phases ago (K(i+2), V(i+1), read from MFMA(i+1) on) have
     // landed before this wave's next barrier: all but its six most recent DMAs are done
     if constexpr (DMA) __builtin_amdgcn_s_waitcnt(0x0F76);  // vmcnt(6)
@@ -384,6 +423,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   };
   // VALU(i): the softmax of tile i
   auto valu_phase = [&](int it) __attribute__((always_inline)) {
+    if constexpr ((F & kFStoresLate) != 0) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): stores landed
     const int cls = tcls(it);
     stamp(3);
     if (cls != 0) softmax(it, cls);
@@ -391,6 +431,11 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     stamp(5);
   };
 
+  uint64_t wg_t1 = 0, wg_c1 = 0, wg_t2 = 0, wg_c2 = 0;
+  if constexpr ((F & kFStampWG) != 0) {
+    wg_t1 = __builtin_amdgcn_s_memrealtime();
+    wg_c1 = __builtin_amdgcn_s_memtime();
+  }
   // Both groups run the same loop (one code path keeps the register allocation sane); group 1
   // enters it one barrier late and group 0 leaves it one barrier late, so every barrier
   // interval pairs one group's MFMA(i) with the other's VALU phase.
@@ -420,6 +465,10 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     }
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();
+  if constexpr ((F & kFStampWG) != 0) {
+    wg_t2 = __builtin_amdgcn_s_memrealtime();
+    wg_c2 = __builtin_amdgcn_s_memtime();
+  }
 
   // ---- epilogue
   if (!wave_active) return;
@@ -445,6 +494,19 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     } else {
       lo[qi] = 0.f;
       mo[qi] = neg_inf_approx<__half>();
+    }
+  }
+  if constexpr ((F & kFStampWG) != 0) {  // diagnostic build: wave 0's timeline over the block's l
+    const uint64_t t3 = __builtin_amdgcn_s_memrealtime(), c3 = __builtin_amdgcn_s_memtime();
+    const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804), xcc = __builtin_amdgcn_s_getreg(0xF814);
+    const uint32_t vals[10] = {(uint32_t)wg_t0, (uint32_t)(wg_t0 >> 32), (uint32_t)(wg_t1 - wg_t0), (uint32_t)(wg_t2 - wg_t0),
+                               (uint32_t)(t3 - wg_t0), (uint32_t)(wg_c1 - wg_c0), (uint32_t)(wg_c2 - wg_c0),
+                               (uint32_t)(c3 - wg_c0), hw, xcc};
+    if (w == 0 && lane < 10) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 10; ++k) v = (lane == k) ? vals[k] : v;
+      reinterpret_cast<uint32_t*>(a.l)[bi * (int64_t)nq + q0 + lane] = v;
     }
   }
   if constexpr ((F & kFStamp) != 0) {  // diagnostic build: stamps over this wave's first l entries
@@ -475,6 +537,7 @@ bool fwd_f16_pingpong_supported(const FwdArgs& a) {
   const int nk = a.rule.k.n;
   const int dm = max(a.d, a.v_d);
   return dm > 32 && dm <= kD && (nk % 8 == 0) && nk > 0 && (int64_t)dm * nk * 2 < (1ll << 31) &&
+         (int64_t)a.d * a.rule.q.n * 2 < (1ll << 31) &&
          (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) && (reinterpret_cast<uintptr_t>(a.V) % 16 == 0) &&
          rule_is_interval(a.rule) && a.b * ((a.rule.q.n + kBM - 1) / kBM) < (1ll << 31);
 }
@@ -484,6 +547,11 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
   switch (ev ? atoi(ev) : -1) {
     case 2200: return launch_t<0>(a, s);
     case 2203: return launch_t<kFPrio | kFStamp>(a, s);
+    case 2204: return launch_t<kFPrio | kFStampWG>(a, s);
+    case 2206: return launch_t<kFPrio | kFStoresLate>(a, s);
+    case 2274: return launch_t<kFPrio | kFStampWG | kANoLoad | kANoStore | kANoFrag>(a, s);
+    case 2275: return launch_t<kFPrio | kFStampWG | kANoExp | kANoMax | kANoSums>(a, s);
+    case 2276: return launch_t<kFPrio | kFStampWG | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
     case 2212: return launch_t<kFPrio | kFDma>(a, s);
     case 2205: return launch_t<kFPrio | kFSumsLate>(a, s);
     case 2211: return launch_t<kFPrio | kFStamp | kANoExp>(a, s);
@@ -496,7 +564,9 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2266: return launch_t<kFPrio | kANoFrag>(a, s);
     case 2267: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag>(a, s);
     case 2268: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
-    default: return launch_t<kFPrio>(a, s);  // tuned (c2, MI355X): MFMA phases at priority 1
+    case 2201: return launch_t<kFPrio>(a, s);
+    // tuned (c2, MI355X): MFMA phases at priority 1, staging stores after the MFMAs (0.3-0.5%)
+    default: return launch_t<kFPrio | kFStoresLate>(a, s);
   }
 }
 
