@@ -336,9 +336,10 @@ def test_config5_full2d_f32_sampled():
 # FA_FWD_VARIANT / FA_BWD_VARIANT pick the opt-in structures the dispatcher does not choose by
 # default; each must stay parity-green on every rule it accepts:
 #   2000 paired-block forward, 2200 ping-pong forward without priority flips, 2201 ping-pong
-#   with priority flips only, 2206 the ping-pong default (staging stores after the MFMAs; forced
-#   here for causal / local too), 2212 ping-pong with LDS-DMA staging, 1814 the 8-wave forward
-#   that the ping-pong kernel replaced, and
+#   with priority flips only, 2206 staging stores after the MFMAs, 2207 / 2208 fragment reads
+#   interleaved with the MFMAs (pairs / single MFMAs), 2213 the ping-pong default (2207 with the
+#   staging pinned too; forced here for causal / local, where the interleave is off), 2212
+#   ping-pong with LDS-DMA staging, 1814 the 8-wave forward that the ping-pong kernel replaced, and
 #   bwd 1281 the software-pipelined dK/dV pass (d = 128).
 VARIANT_CASES = [
     ("full", 1, "none_front", (264,), (136,), 1, False, 64, 64),
@@ -351,7 +352,7 @@ VARIANT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", ["2000", "2200", "2201", "2206", "2212", "1814"])
+@pytest.mark.parametrize("variant", ["2000", "2200", "2201", "2206", "2207", "2208", "2212", "2213", "1814"])
 @pytest.mark.parametrize("policy,seq_dims,mode,qs,ks,ws,causal,d,vd", VARIANT_CASES)
 def test_f16_forward_structures(monkeypatch, variant, policy, seq_dims, mode, qs, ks, ws, causal, d, vd):
     monkeypatch.setenv("FA_FWD_VARIANT", variant)

@@ -71,6 +71,15 @@ constexpr int kFStampWG = 2048;
 // the MFMA phase's staging stores after its MFMAs and fragment reads (their vmcnt waits and
 // store-path cycles under the running PV MFMAs); lgkmcnt(0) at the start of the VALU phase
 constexpr int kFStoresLate = 4096;
+// full policy: the K(i+1) / V(i) fragment reads interleaved with the MFMAs that free their
+// registers (sched_group_barrier), so the four waves of a group spread their LDS traffic over the
+// phase instead of bursting it between the Sᵀ and PV MFMAs.  The MFMAs become unconditional: P is
+// zeroed for a skipped tile and V's fragments start at zero.
+constexpr int kFInterleave = 8192;
+constexpr int kFIlvFine = 16384;  // ... one MFMA at a time (2 / 1 reads after each)
+constexpr int kFIlvStores = 32768;  // ... and the staging stores / loads pinned after the 2nd MFMA pair of each half
+constexpr int kFIlvAt0 = 65536;     // ... (after the 1st pair)
+constexpr int kFIlvAt2 = 131072;    // ... (after the 3rd pair)
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
@@ -250,6 +259,15 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
 
   half8 kf[2][4];  // K fragments for the next Sᵀ
   half8 vf[4][2];  // V fragments for the next PV
+  constexpr bool ILV = (F & kFInterleave) != 0 && POL == 0 && !DMA;
+  if constexpr (ILV) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vf[s][u][e] = (_Float16)0.f;
+  }
   auto read_k = [&](int slot) __attribute__((always_inline)) {
     const lds_char_t* p = smem + kOffK + slot * kTile;
 #pragma unroll
@@ -273,6 +291,12 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
                        // bit-cast half8 miscompiles with this toolchain)
   floatx16 o[2];       // Oᵀ: channels 32u + 8(i>>2) + 4h + (i&3)
   floatx16 negm;       // -m_run broadcast: the C operand of every Sᵀ chain
+  if constexpr (ILV) {  // PV(-1) runs unconditionally: P starts at zero
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) pw[x][y] = 0u;
+  }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     o[0][i] = 0.f;
@@ -377,15 +401,70 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
       }
     }
-    if (tcls(it) != 0) {
+    if constexpr (ILV) {
+      const lds_char_t* pk = smem + kOffK + ((c + 1) % kNS) * kTile;
+      const lds_char_t* pv = smem + kOffV + c * kTile;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], qf[s], s == 0 ? negm : st[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          kf[t][s].lo = tr_read(pk + kbase[t] + (16 * s) * 128);
+          kf[t][s].hi = tr_read(pk + kbase[t] + (16 * s + 4) * 128);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const half8 p = __builtin_bit_cast(half8, u32x4{pw[s][0], pw[s][1], pw[s][2], pw[s][3]});
+#pragma unroll
+        for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[u], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) vf[s][u] = read_b128(pv + vbase[s] + 32 * u * 128);
+      }
+      constexpr int kIlvAt = (F & kFIlvAt0) ? 0 : (F & kFIlvAt2) ? 2 : 1;
+      if constexpr ((F & kFIlvFine) != 0) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+          if constexpr ((F & kFIlvStores) != 0) {
+            if (s == kIlvAt) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // a staging store
+            if (s == kIlvAt) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // a staging load
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          if constexpr ((F & kFIlvStores) != 0) {
+            if (s == kIlvAt) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            if (s == kIlvAt) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          }
+        }
+      }
+    }
+    if (!ILV && tcls(it) != 0) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
           st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], qf[s], s == 0 ? negm : st[t], 0, 0, 0);
     }
-    if (!(F & kANoFrag)) read_k((c + 1) % kNS);
-    if (tcls(it - 1) != 0) {
+    if (!ILV && !(F & kANoFrag)) read_k((c + 1) % kNS);
+    if (!ILV && tcls(it - 1) != 0) {
       if (F & kFSumsLate) row_sums();
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -394,7 +473,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[u], 0, 0, 0);
       }
     }
-    if (!(F & kANoFrag)) read_v(c);
+    if (!ILV && !(F & kANoFrag)) read_v(c);
     if constexpr ((F & kFStoresLate) != 0 && !DMA) {
       store(kOffK + c * kTile + kwo, kst[c]);
       store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
@@ -427,6 +506,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     const int cls = tcls(it);
     stamp(3);
     if (cls != 0) softmax(it, cls);
+    if constexpr (ILV) {
+      if (cls == 0) {  // the next (unconditional) PV must add nothing
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y) pw[x][y] = 0u;
+      }
+    }
     stamp(4);
     stamp(5);
   };
@@ -549,6 +636,14 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2203: return launch_t<kFPrio | kFStamp>(a, s);
     case 2204: return launch_t<kFPrio | kFStampWG>(a, s);
     case 2206: return launch_t<kFPrio | kFStoresLate>(a, s);
+    case 2207: return launch_t<kFPrio | kFStoresLate | kFInterleave>(a, s);
+    case 2208: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvFine>(a, s);
+    case 2209: return launch_t<kFPrio | kFInterleave>(a, s);
+    case 2210: return launch_t<kFInterleave | kFStoresLate>(a, s);
+    case 2213: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores>(a, s);
+    case 2214: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores | kFIlvAt0>(a, s);
+    case 2215: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores | kFIlvAt2>(a, s);
+    case 2216: return launch_t<kFStoresLate | kFInterleave | kFIlvStores>(a, s);
     case 2274: return launch_t<kFPrio | kFStampWG | kANoLoad | kANoStore | kANoFrag>(a, s);
     case 2275: return launch_t<kFPrio | kFStampWG | kANoExp | kANoMax | kANoSums>(a, s);
     case 2276: return launch_t<kFPrio | kFStampWG | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
@@ -565,8 +660,9 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2267: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag>(a, s);
     case 2268: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
     case 2201: return launch_t<kFPrio>(a, s);
-    // tuned (c2, MI355X): MFMA phases at priority 1, staging stores after the MFMAs (0.3-0.5%)
-    default: return launch_t<kFPrio | kFStoresLate>(a, s);
+    // tuned (c2, MI355X): MFMA phases at priority 1, fragment reads and staging interleaved with
+    // the MFMAs (full policy; 0.5526-0.5716 ms against 0.595 for 2206)
+    default: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores>(a, s);
   }
 }
 
