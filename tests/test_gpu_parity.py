@@ -369,6 +369,16 @@ def test_f16_forward_structures_d128(monkeypatch, variant, policy, seq_dims, mod
              bwd=False, seed=int(variant) + d + ws)
 
 
+# backward operand-read placement: 1200 = the d = 128 passes with reads beside their MFMAs (the
+# default before the run-ahead reads), 1069 = the d <= 64 passes with run-ahead reads
+@pytest.mark.parametrize("variant,d", [("1200", 128), ("1069", 64), ("1069", 48)])
+@pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, True)])
+def test_f16_backward_read_placement(monkeypatch, variant, d, policy, ws, causal):
+    monkeypatch.setenv("FA_BWD_VARIANT", variant)
+    run_case(np.float16, policy, 1, "none_front", (2,), d, d, (328,), (264,), ws=ws, ls=0, causal=causal,
+             seed=int(variant) + d)
+
+
 @pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, False)])
 def test_f16_backward_pipelined_dkdv(monkeypatch, policy, ws, causal):
     monkeypatch.setenv("FA_BWD_VARIANT", "1281")

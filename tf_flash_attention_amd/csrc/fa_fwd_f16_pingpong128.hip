@@ -113,10 +113,18 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
     load(k0v, krs, koff, kt0);
     load(k1v, krs, koff, kt0 + kBN);
     load(v0v, vrs, voff, kt0);
-    for (int idx = tid; idx < kD * (kBM / 8); idx += kNW * 64) {  // Q [128][256], 64-B blocks XOR-swizzled by c&3
-      const int c = idx / (kBM / 8), m = idx % (kBM / 8);
-      const u32x4 v = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec) : u32x4{0, 0, 0, 0};
-      *reinterpret_cast<lds_u32x4_t*>(smem + c * kQRow + ((m * 16) ^ ((c & 3) << 6))) = v;
+    // Q [128][256], 64-B blocks XOR-swizzled by c&3: all of a thread's loads before its stores
+    constexpr int kQPT = kD * (kBM / 8) / (kNW * 64);
+    u32x4 qv[kQPT];
+#pragma unroll
+    for (int j = 0; j < kQPT; ++j) {
+      const int idx = tid + j * kNW * 64, c = idx / (kBM / 8), m = idx % (kBM / 8);
+      qv[j] = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int j = 0; j < kQPT; ++j) {
+      const int idx = tid + j * kNW * 64, c = idx / (kBM / 8), m = idx % (kBM / 8);
+      *reinterpret_cast<lds_u32x4_t*>(smem + c * kQRow + ((m * 16) ^ ((c & 3) << 6))) = qv[j];
     }
     store(kOffK, kwo, k0v);
     store(kOffK + kTile, kwo, k1v);
