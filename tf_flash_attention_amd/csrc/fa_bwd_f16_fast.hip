@@ -253,25 +253,26 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   // ABL bit 64 (not an ablation): the operand reads of sdp / dvdk run two k-steps ahead of their
   // MFMAs (one wave per SIMD: nothing else hides an LDS round trip between a read and its MFMA)
   constexpr bool PRE = (ABL & 64) != 0;
+  constexpr int kAh = (ABL & 128) ? 3 : 2;  // run-ahead distance (MFMA pairs)
   // S = Qᵀ·K', dP = dOᵀ·V: A operands (row q, k = channel) by transposed reads
   auto sdp_pre = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) __attribute__((always_inline)) {
     constexpr int kS = D / 16;
-    half8 qa8[3], oa8[3];
+    half8 qa8[kAh + 1], oa8[kAh + 1];
     auto rd = [&](int s) __attribute__((always_inline)) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const uint32_t off = q16_off(16 * s + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
         const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
-        if (e == 0) { qa8[s % 3].lo = x; oa8[s % 3].lo = y; } else { qa8[s % 3].hi = x; oa8[s % 3].hi = y; }
+        if (e == 0) { qa8[s % (kAh + 1)].lo = x; oa8[s % (kAh + 1)].lo = y; } else { qa8[s % (kAh + 1)].hi = x; oa8[s % (kAh + 1)].hi = y; }
       }
     };
-    rd(0);
-    rd(1);
+#pragma unroll
+    for (int s = 0; s < kAh; ++s) rd(s);
 #pragma unroll
     for (int s = 0; s < kS; ++s) {
-      if (s + 2 < kS) rd(s + 2);
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8[s % 3], kb[s], sacc, 0, 0, 0);
-      pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8[s % 3], vb[s], pacc, 0, 0, 0);
+      if (s + kAh < kS) rd(s + kAh);
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8[s % (kAh + 1)], kb[s], sacc, 0, 0, 0);
+      pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8[s % (kAh + 1)], vb[s], pacc, 0, 0, 0);
     }
   };
   auto sdp = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) {
@@ -314,20 +315,20 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   auto dvdk = [&](const lds_char_t* base, const half8 (&pf)[2], const half8 (&sf)[2]) {
     if constexpr (PRE) {
       constexpr int kU = D / 32, kN = 2 * kU;  // (s, u) pairs, n = s * kU + u
-      half8 oa[3], qa[3];
+      half8 oa[kAh + 1], qa[kAh + 1];
       auto rd = [&](int n) __attribute__((always_inline)) {
         const int s_ = n / kU, u = n % kU;
-        oa[n % 3] = read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s_ + h));
-        qa[n % 3] = read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s_ + h));
+        oa[n % (kAh + 1)] = read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s_ + h));
+        qa[n % (kAh + 1)] = read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s_ + h));
       };
-      rd(0);
-      rd(1);
+#pragma unroll
+      for (int n = 0; n < kAh; ++n) rd(n);
 #pragma unroll
       for (int n = 0; n < kN; ++n) {
-        if (n + 2 < kN) rd(n + 2);
+        if (n + kAh < kN) rd(n + kAh);
         const int s_ = n / kU, u = n % kU;
-        dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa[n % 3], pf[s_], dv[u], 0, 0, 0);
-        dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[n % 3], sf[s_], dk[u], 0, 0, 0);
+        dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa[n % (kAh + 1)], pf[s_], dv[u], 0, 0, 0);
+        dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[n % (kAh + 1)], sf[s_], dk[u], 0, 0, 0);
       }
       return;
     }
@@ -764,6 +765,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
     case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
     case 1200: e = launch_dkdv<128, 4, 1>(a, s); break;  // operand reads not run ahead (before the default)
     case 1264: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
+    case 1267: e = launch_dkdv<128, 4, 1, false, 64 | 128>(a, s); break;
     case 1301: e = launch_dkdv<128, 4, 1, false, 1>(a, s); break;
     case 1302: e = launch_dkdv<128, 4, 1, false, 2>(a, s); break;
     case 1304: e = launch_dkdv<128, 4, 1, false, 4>(a, s); break;
