@@ -158,10 +158,31 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_ke
 #pragma unroll
     for (int x = 0; x < TPB; ++x)
       if (x < ntiles) load_into(pv[x], vrs, kt0 + x * kBN, vd);
-    for (int idx = tid; idx < D * (kBM / 8); idx += kThr) {  // Q [D][BM], 64-B blocks XOR-swizzled by c&3
-      const int c = idx / (kBM / 8), m = idx % (kBM / 8);
-      const u32x4 v = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, qvec) : u32x4{0, 0, 0, 0};
-      *reinterpret_cast<lds_u32x4_t*>(smem + c * S::kQRow + ((m * 16) ^ ((c & 3) << 6))) = v;
+    // Q [D][BM], 64-B blocks XOR-swizzled by c&3: all of a thread's chunks loaded before any is
+    // stored (a rolled loop serialised D/16 memory latencies in every block's prologue)
+    constexpr int kQPT = D * (kBM / 8) / kThr;
+    static_assert(kQPT * kThr == D * (kBM / 8), "Q chunks must divide over the workgroup");
+    u32x4 qv[kQPT];
+    if (qvec) {  // branch-free buffer loads (chunks past d or nq read as zeros)
+      const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Q, 2u * d * nq);
+#pragma unroll
+      for (int j = 0; j < kQPT; ++j) {
+        const int idx = tid + j * kThr, c = idx / (kBM / 8), m = idx % (kBM / 8);
+        const bool in = c < d && q0 + 8 * m < nq;
+        qv[j] = __builtin_amdgcn_raw_buffer_load_b128(qrs, in ? (uint32_t)c * (uint32_t)nq * 2u + 16u * m : 0x80000000u,
+                                                      2 * q0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kQPT; ++j) {
+        const int idx = tid + j * kThr, c = idx / (kBM / 8), m = idx % (kBM / 8);
+        qv[j] = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, false) : u32x4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kQPT; ++j) {
+      const int idx = tid + j * kThr, c = idx / (kBM / 8), m = idx % (kBM / 8);
+      *reinterpret_cast<lds_u32x4_t*>(smem + c * S::kQRow + ((m * 16) ^ ((c & 3) << 6))) = qv[j];
     }
 #pragma unroll
     for (int x = 0; x <= TPB; ++x)
@@ -474,9 +495,9 @@ bool fwd_f16_fast_supported(const FwdArgs& a) {
   const int nk = a.rule.k.n;
   const int dm = max(a.d, a.v_d);
   return dm > 32 && dm <= 128 && (nk % 8 == 0) && nk > 0 &&
-         (int64_t)dm * nk * 2 < (1ll << 31) && (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) &&
-         (reinterpret_cast<uintptr_t>(a.V) % 16 == 0) && rule_is_interval(a.rule) &&
-         a.b * ((a.rule.q.n + 127) / 128) < (1ll << 31);
+         (int64_t)dm * nk * 2 < (1ll << 31) && (int64_t)a.d * a.rule.q.n * 2 < (1ll << 31) &&
+         (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) && (reinterpret_cast<uintptr_t>(a.V) % 16 == 0) &&
+         rule_is_interval(a.rule) && a.b * ((a.rule.q.n + 127) / 128) < (1ll << 31);
 }
 
 hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
