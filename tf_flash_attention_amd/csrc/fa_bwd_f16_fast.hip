@@ -137,13 +137,26 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   // ---- resident B operands: lane (r,h) holds X[c = 16s + 8h + j][key = k0 + 32w + r]
   half8 kb[D / 16], vb[D / 16];
   {
-    for (int idx = tid; idx < 2 * D * (kBK / 8); idx += kThr) {
-      const int which = idx >= D * (kBK / 8);
-      const int j = which ? idx - D * (kBK / 8) : idx;
+    // every chunk of a thread loaded before any is stored, branch-free (chunks past the channel
+    // count or nk read as zeros): a rolled load-store loop here serialised 2D/16 memory
+    // latencies in every block's prologue
+    constexpr int kRPT = 2 * D * (kBK / 8) / kThr, kHalf = D * (kBK / 8) / kThr;
+    static_assert(kHalf * kThr == D * (kBK / 8), "resident chunks must divide over the workgroup");
+    const __amdgpu_buffer_rsrc_t krs2 = make_rsrc(K, 2u * d * nk), vrs2 = make_rsrc(V, 2u * vd * nk);
+    u32x4 rv[kRPT];
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
       const int c = j / (kBK / 8), m = j % (kBK / 8);
-      const u32x4 v = (c < (which ? vd : d)) ? load_chunk8((which ? V : K) + (int64_t)c * nk, k0 + 8 * m, nk, true)
-                                              : u32x4{0, 0, 0, 0};
-      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBK) + ((m * 16) ^ ((c & 3) << 6))) = v;
+      const bool in = c < (which ? vd : d) && k0 + 8 * m < nk;
+      rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? vrs2 : krs2,
+                                                     in ? (uint32_t)c * (uint32_t)nk * 2u + 16u * m : 0x80000000u, 2 * k0, 0);
+    }
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
+      const int c = j / (kBK / 8), m = j % (kBK / 8);
+      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBK) + ((m * 16) ^ ((c & 3) << 6))) = rv[jj];
     }
     __syncthreads();
 #pragma unroll
@@ -488,13 +501,24 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   // ---- resident B operands: lane (r,h) holds X[c = 16s + 8h + j][q = wq0 + r]
   half8 qf[D / 16], of[D / 16];
   {
-    for (int idx = tid; idx < 2 * D * (kBM / 8); idx += kThr) {
-      const int which = idx >= D * (kBM / 8);
-      const int j = which ? idx - D * (kBM / 8) : idx;
+    // all loads before the stores, branch-free (see the dK/dV pass)
+    constexpr int kRPT = 2 * D * (kBM / 8) / kThr, kHalf = D * (kBM / 8) / kThr;
+    static_assert(kHalf * kThr == D * (kBM / 8), "resident chunks must divide over the workgroup");
+    const __amdgpu_buffer_rsrc_t qrs2 = make_rsrc(Q, 2u * d * nq), ors2 = make_rsrc(dO, 2u * vd * nq);
+    u32x4 rv[kRPT];
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
       const int c = j / (kBM / 8), m = j % (kBM / 8);
-      const u32x4 v = (c < (which ? vd : d)) ? load_chunk8((which ? dO : Q) + (int64_t)c * nq, q0 + 8 * m, nq, true)
-                                              : u32x4{0, 0, 0, 0};
-      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBM) + ((m * 16) ^ ((c & 3) << 6))) = v;
+      const bool in = c < (which ? vd : d) && q0 + 8 * m < nq;
+      rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? ors2 : qrs2,
+                                                     in ? (uint32_t)c * (uint32_t)nq * 2u + 16u * m : 0x80000000u, 2 * q0, 0);
+    }
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
+      const int c = j / (kBM / 8), m = j % (kBM / 8);
+      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBM) + ((m * 16) ^ ((c & 3) << 6))) = rv[jj];
     }
     __syncthreads();
 #pragma unroll
