@@ -411,6 +411,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
           st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], qf[s], s == 0 ? negm : st[t], 0, 0, 0);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
+          if (F & kANoFrag) break;
           kf[t][s].lo = tr_read(pk + kbase[t] + (16 * s) * 128);
           kf[t][s].hi = tr_read(pk + kbase[t] + (16 * s + 4) * 128);
         }
@@ -421,7 +422,8 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
 #pragma unroll
         for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[u], 0, 0, 0);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) vf[s][u] = read_b128(pv + vbase[s] + 32 * u * 128);
+        for (int u = 0; u < 2; ++u)
+          if (!(F & kANoFrag)) vf[s][u] = read_b128(pv + vbase[s] + 32 * u * 128);
       }
       constexpr int kIlvAt = (F & kFIlvAt0) ? 0 : (F & kFIlvAt2) ? 2 : 1;
       if constexpr ((F & kFIlvFine) != 0) {
@@ -475,10 +477,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     }
     if (!ILV && !(F & kANoFrag)) read_v(c);
     if constexpr ((F & kFStoresLate) != 0 && !DMA) {
-      store(kOffK + c * kTile + kwo, kst[c]);
-      store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
-      kst[c] = load(krs, koff, kt0 + (it + 6) * kBN);
-      vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
+      if (!(F & kANoStore)) {
+        store(kOffK + c * kTile + kwo, kst[c]);
+        store(kOffV + ((c + 2) % kNS) * kTile + vwo, vst[c]);
+      }
+      if (!(F & kANoLoad)) {
+        kst[c] = load(krs, koff, kt0 + (it + 6) * kBN);
+        vst[c] = load(vrs, voff, kt0 + (it + 5) * kBN);
+      }
     }
     // DMA: the tiles issued three MFMA phases ago (K(i+2), V(i+1), read from MFMA(i+1) on) have
     // landed before this wave's next barrier: all but its six most recent DMAs are done
@@ -647,6 +653,10 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2274: return launch_t<kFPrio | kFStampWG | kANoLoad | kANoStore | kANoFrag>(a, s);
     case 2275: return launch_t<kFPrio | kFStampWG | kANoExp | kANoMax | kANoSums>(a, s);
     case 2276: return launch_t<kFPrio | kFStampWG | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
+    case 2277: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores | kFStampWG>(a, s);
+    case 2278: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores | kFStampWG | kANoLoad | kANoStore | kANoFrag>(a, s);
+    case 2279: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores | kFStampWG | kANoExp | kANoMax | kANoSums>(a, s);
+    case 2280: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores | kFStampWG | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
     case 2212: return launch_t<kFPrio | kFDma>(a, s);
     case 2205: return launch_t<kFPrio | kFSumsLate>(a, s);
     case 2211: return launch_t<kFPrio | kFStamp | kANoExp>(a, s);
