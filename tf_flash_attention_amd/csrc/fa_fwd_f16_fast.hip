@@ -448,13 +448,26 @@ __global__ __launch_bounds__(NW * 64, fast_waves_per_eu(D)) void fwd_f16_fast_ke
   const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
   if (qi < nq) {
     __half* O = static_cast<__half*>(a.O) + bi * (int64_t)vd * nq;
+    if (vd == D) {  // one buffer store per value, no per-store address / predicate (see the ping-pong kernel)
+      const __amdgpu_buffer_rsrc_t ors = make_rsrc(O, 2u * vd * nq);
+      const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nq + (uint32_t)qi);
 #pragma unroll
-    for (int u = 0; u < D / 32; ++u)
+      for (int u = 0; u < D / 32; ++u)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int v = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (v < vd) O[(int64_t)v * nq + qi] = __float2half(acc_o[u][i] * inv);
-      }
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t cst = 32u * u + (i & 3) + 8u * (i >> 2);
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(acc_o[u][i] * inv)), ors,
+                                                vlane, 2u * cst * (uint32_t)nq, 0);
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int v = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (v < vd) O[(int64_t)v * nq + qi] = __float2half(acc_o[u][i] * inv);
+        }
+    }
     if (h == 0) {
       float* lo = static_cast<float*>(a.l) + bi * (int64_t)nq;
       __half* mo = static_cast<__half*>(a.m) + bi * (int64_t)nq;
@@ -495,7 +508,7 @@ bool fwd_f16_fast_supported(const FwdArgs& a) {
   const int nk = a.rule.k.n;
   const int dm = max(a.d, a.v_d);
   return dm > 32 && dm <= 128 && (nk % 8 == 0) && nk > 0 &&
-         (int64_t)dm * nk * 2 < (1ll << 31) && (int64_t)a.d * a.rule.q.n * 2 < (1ll << 31) &&
+         (int64_t)dm * nk * 2 < (1ll << 31) && (int64_t)dm * a.rule.q.n * 2 < (1ll << 31) &&
          (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) && (reinterpret_cast<uintptr_t>(a.V) % 16 == 0) &&
          rule_is_interval(a.rule) && a.b * ((a.rule.q.n + 127) / 128) < (1ll << 31);
 }

@@ -569,13 +569,29 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
   if (qi >= nq) return;
   __half* O = static_cast<__half*>(a.O) + bi * (int64_t)vd * nq;
+  if (vd == kD) {
+    // every channel in range: one buffer store per value, the lane's offset in a VGPR and the
+    // channel's in an SGPR (the generic form below spends a 64-bit address, a compare and an
+    // exec branch on each of the 32 stores)
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(O, 2u * vd * nq);
+    const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nq + (uint32_t)qi);
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int v = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-      if (v < vd) O[(int64_t)v * nq + qi] = __float2half(o[u][i] * inv);
-    }
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t cst = 32u * u + (i & 3) + 8u * (i >> 2);
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(o[u][i] * inv)), ors, vlane,
+                                              2u * cst * (uint32_t)nq, 0);
+      }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int v = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (v < vd) O[(int64_t)v * nq + qi] = __float2half(o[u][i] * inv);
+      }
+  }
   if (h == 0) {
     float* lo = static_cast<float*>(a.l) + bi * (int64_t)nq;
     __half* mo = static_cast<__half*>(a.m) + bi * (int64_t)nq;
@@ -630,7 +646,7 @@ bool fwd_f16_pingpong_supported(const FwdArgs& a) {
   const int nk = a.rule.k.n;
   const int dm = max(a.d, a.v_d);
   return dm > 32 && dm <= kD && (nk % 8 == 0) && nk > 0 && (int64_t)dm * nk * 2 < (1ll << 31) &&
-         (int64_t)a.d * a.rule.q.n * 2 < (1ll << 31) &&
+         (int64_t)dm * a.rule.q.n * 2 < (1ll << 31) &&
          (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) && (reinterpret_cast<uintptr_t>(a.V) % 16 == 0) &&
          rule_is_interval(a.rule) && a.b * ((a.rule.q.n + kBM - 1) / kBM) < (1ll << 31);
 }
