@@ -441,6 +441,20 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   __half* dK = static_cast<__half*>(a.dK) + bi * (int64_t)d * nk;
   __half* dV = static_cast<__half*>(a.dV) + bi * (int64_t)vd * nk;
   const float sc = (float)a.scale;
+  if (d == D && vd == D) {  // one buffer store per value, the row's offset in an SGPR (no per-store
+                            // 64-bit address, compare or exec branch)
+    const __amdgpu_buffer_rsrc_t krs_ = make_rsrc(dK, 2u * d * nk), vrs_ = make_rsrc(dV, 2u * vd * nk);
+    const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nk + (uint32_t)key);
+#pragma unroll
+    for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t so = 2u * (32u * u + (i & 3) + 8u * (i >> 2)) * (uint32_t)nk;
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(dk[u][i] * sc)), krs_, vlane, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)dv[u][i]), vrs_, vlane, so, 0);
+      }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < D / 32; ++u)
 #pragma unroll
@@ -716,6 +730,17 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   if (!wave_active || qi >= nq) return;
   __half* dQ = static_cast<__half*>(a.dQ) + bi * (int64_t)d * nq;
   const float sc = (float)a.scale;
+  if (d == D) {  // one buffer store per value (see the dK/dV pass)
+    const __amdgpu_buffer_rsrc_t qrs_ = make_rsrc(dQ, 2u * d * nq);
+    const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nq + (uint32_t)qi);
+#pragma unroll
+    for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(dq[u][i] * sc)), qrs_, vlane,
+                                              2u * (32u * u + (i & 3) + 8u * (i >> 2)) * (uint32_t)nq, 0);
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < D / 32; ++u)
 #pragma unroll
