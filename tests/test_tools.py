@@ -1,0 +1,40 @@
+"""CPU checks of the assembly hazard scanner (tools/check_store_hazard.py): a
+>8-byte vector-memory store whose data VGPRs the very next VALU instruction overwrites."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOL = os.path.join(ROOT, "tools", "check_store_hazard.py")
+
+HAZARD = """_Zkernel:
+	buffer_store_dwordx4 v[2:5], v14, s[24:27], s19 offen
+	v_ashrrev_i32_e32 v2, 2, v13
+	s_endpgm
+"""
+CLEAN = """_Zkernel:
+	buffer_store_dwordx4 v[2:5], v14, s[24:27], s19 offen
+	; sched_barrier mask(0x00000000)
+	s_nop 1
+	v_ashrrev_i32_e32 v2, 2, v13
+	global_store_dwordx2 v[6:7], v[0:1], off
+	v_lshl_add_u64 v[0:1], s[0:1], 0, v[4:5]
+	s_endpgm
+"""
+
+
+def _run(tmp_path, text):
+    f = tmp_path / "k.s"
+    f.write_text(text)
+    return subprocess.run([sys.executable, TOOL, str(f)], capture_output=True, text=True)
+
+
+def test_store_hazard_detected(tmp_path):
+    r = _run(tmp_path, HAZARD)
+    assert r.returncode == 1 and "1 hazard pair(s)" in r.stdout
+
+
+def test_store_hazard_clean(tmp_path):
+    # a wait state in between, and an 8-byte store (not affected) followed by a write of its data
+    r = _run(tmp_path, CLEAN)
+    assert r.returncode == 0 and "0 hazard pair(s)" in r.stdout
