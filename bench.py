@@ -6,9 +6,12 @@ B=8 H=16 d=64 Nq=Nk=4096, forward — metric "fwd TFLOP/s per GPU + MFMA util %"
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--no-cpu-baseline]
 
-For N>1 run under torch.distributed.run: one process per GPU, each rank runs
-its own shard of batch×head slices (no data-path collective; a gloo
-barrier / max-reduce over CPU tensors only brackets the timed region).
+For N>1: one process per GPU, each rank runs its own shard of batch×head
+slices (no data-path collective; a gloo barrier / max-reduce over CPU tensors
+only brackets the timed region).  Under torch.distributed.run the ranks come
+from the environment; without it (WORLD_SIZE unset) `--gpus N` starts N fresh
+child processes itself, before anything touches the GPU, and exits with the
+worst child's status.
 c2/c3/c5: every rank processes the full config batch (weak scaling);
 c4: the config's b=1024 slices are split across ranks (strong scaling, as the
 config prescribes "batch-sharded across 8×MI355X").
@@ -22,6 +25,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -31,7 +35,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from tf_flash_attention_amd import flash_attention as fa  # noqa: E402
+from tf_flash_attention_amd import flash_attention as fa  # noqa: E402  (the HIP library loads lazily)
 from tf_flash_attention_amd import shard  # noqa: E402
 
 MFMA_PEAK = {"fp16": 2516.6, "fp32": 157.3, "fp64": 78.6}   # dense TFLOP/s (MI355X_MICROARCH.md)
@@ -70,7 +74,7 @@ def cpu_baseline(cfg, budget_s: float):
     from oracle import fa_oracle as O
     try:
         from threadpoolctl import threadpool_info
-        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])  # BLAS threads actually used
     except Exception:  # pragma: no cover
         cores = 1
     policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, _ = cfg
@@ -95,8 +99,40 @@ def cpu_baseline(cfg, budget_s: float):
             break
     tflops = flops_slice * n / el / 1e12
     return {"value": tflops, "unit": "TFLOP/s", "cores": int(cores), "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": _cpu_model(),
             "sample": f"{n} of {int(np.prod(batch))} (b,h) slices of the workload, numpy fp32 naive attention "
                       f"(einsum->softmax->einsum, tests/test_1d.py:69-76), {el:.1f}s; fp16 inputs upcast"}
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:  # pragma: no cover
+        pass
+    return "unknown"
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start `n` fresh bench processes (RANK/WORLD_SIZE/LOCAL_RANK set, gloo rendezvous on
+    127.0.0.1) and wait for them.  Called only from a parent that has not touched the GPU:
+    the children initialise HIP themselves (rank r on GPU r % device_count).  Returns the
+    worst exit status."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
 
 
 def algorithmic_bytes(cfg, b):
@@ -120,24 +156,30 @@ def load_traffic(workload_key: str):
     path = os.path.join(ROOT, "profiles", f"traffic_{workload_key}.json")
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            t = json.load(f)
+        return t.get("hbm_bytes_per_launch"), t.get("algorithmic_read_bytes", 0) + t.get("algorithmic_write_bytes", 0)
     except Exception:
-        return None
+        return None, 0
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    # the first ~20 launches on a fresh box run ~15 % slow (clock ramp); 40 untimed steps cover it
     ap.add_argument("--warmup", type=int, default=40)
+    # the chip's clock ramps for the first ~0.5 s of back-to-back launches on a fresh box (c2 at
+    # --warmup 5 ran 0.64 ms/step against 0.57 after the ramp): untimed warm-up continues past the
+    # W steps until this much wall time has gone by; the line reports both
+    ap.add_argument("--warmup-s", type=float, default=1.0)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = shard.dist_env()
-    if world != args.gpus and world > 1:
+    if world != args.gpus:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
     dist = None
     if world > 1:
@@ -178,9 +220,17 @@ def main():
         if bwd:
             _call_backward(cfg, q, k, v, o, l, m, do)
 
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    extra = 0
+    while time.perf_counter() - tw < args.warmup_s:
+        for _ in range(8):
+            step()
+        extra += 8
+        torch.cuda.synchronize()
+    warm_s = time.perf_counter() - tw
 
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -211,9 +261,11 @@ def main():
         dname = DTYPE_NAME[dt]
         peak = MFMA_PEAK[dname]
         achieved = step_flops_rank / (kern_ms * 1e-3) / 1e12  # one rank's launches / event-timed duration
-        traffic = load_traffic(args.config)
+        traffic, traffic_alg = load_traffic(args.config)
         rd, wr = algorithmic_bytes(cfg, b_rank)
         alg_bytes = rd + wr
+        if traffic is not None and traffic_alg and traffic_alg != alg_bytes:
+            traffic = traffic * alg_bytes / traffic_alg  # profiled at another batch: per-slice scaling
         # the binding roof: time at MFMA peak vs time at HBM peak for the algorithmic work
         hbm_bound = alg_bytes / (HBM_PEAK_GBS * 1e9) > step_flops_rank / (peak * 1e12)
         if hbm_bound:
@@ -222,7 +274,11 @@ def main():
         else:
             roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s"}
         roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-        roof.update({"traffic": traffic, "algorithmic_flops_per_launch": step_flops_rank,
+        roof.update({"traffic": traffic,
+                     "traffic_source": f"profiles/traffic_{args.config}.json (rocprofv3 PMC FETCH_SIZE + WRITE_SIZE "
+                                       "of this kernel, committed from a separate profiling run; not measured here)"
+                     if traffic is not None else None,
+                     "algorithmic_flops_per_launch": step_flops_rank,
                      "algorithmic_bytes_per_launch": alg_bytes, "event_ms_per_launch": round(kern_ms, 4)})
         line = {
             "metric": "fwd TFLOP/s per GPU + MFMA util %, fp16 full_1d d=64 seq=4096" if args.config == "c2"
@@ -232,6 +288,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_extra_steps": extra,
+            "warmup_s": round(warm_s, 3),
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": scaling,

@@ -119,6 +119,76 @@ def test_validate_rejects_bad_problems():
     assert L.fa_validate(p) == _lib.FA_ERR_INVALID_ARGUMENT
 
 
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("ls", [0, 1])
+def test_window_near_int32_max_does_not_overflow(causal, ls):
+    """window_size up to INT32_MAX (fa_validate accepts ws << ls <= INT32_MAX): the rule's reach and
+    interval arithmetic must saturate, not wrap (64x64 local gave 128 pairs, not 4096)."""
+    from oracle import fa_oracle as O
+    ws = (2 ** 31 - 1) >> ls
+    L = _lib.lib()
+    for seq_dims, qs, ks in ((1, [64], [64]), (1, [40], [72]), (2, [8, 8], [8, 8])):
+        p = _prob("local", qs, ks, ws=ws, ls=ls, causal=causal)
+        assert L.fa_validate(p) == 0
+        mask = O.problem_mask(O.Problem("local", seq_dims, "none_front", ws, ls, causal), qs, ks)
+        assert L.fa_allowed_pairs(p) == int(mask.sum())
+        np.testing.assert_array_equal(_lib_mask(p, int(np.prod(qs)), int(np.prod(ks))), mask)
+        nq, nk = int(np.prod(qs)), int(np.prod(ks))
+        out = (ctypes.c_int32 * 5)()
+        for q0, q1, k0, k1 in ((0, nq - 1, 0, nk - 1), (3, 9, 10, 20), (nq - 5, nq - 1, 0, 4)):
+            assert L.fa_rule_probe(p, q0, q1, k0, k1, out) == 0
+            kb, ke, qb, qe = out[0], out[1], out[2], out[3]
+            need_k = np.nonzero(mask[q0:q1 + 1].any(axis=0))[0]
+            need_q = np.nonzero(mask[:, k0:k1 + 1].any(axis=1))[0]
+            if need_k.size:
+                assert kb <= need_k.min() and ke > need_k.max()
+            if need_q.size:
+                assert qb <= need_q.min() and qe > need_q.max()
+
+
+def test_library_was_built_from_these_sources():
+    """fa_build_info() carries the hash of the sources the library was compiled from (Makefile
+    SRC_HASH): a stale or foreign libfa_hip.so fails here, on CPU and on the GPU box alike."""
+    info = _lib.build_info()
+    assert f"src={_lib.source_hash()};" in info, (info, _lib.source_hash())
+    assert "lib=product" in info
+
+
+def test_product_library_reads_no_environment():
+    """A/B variants, ablations (outputs WRONG) and stamp builds live only in libfa_hip_diag.so
+    (-DFA_DIAG); the product library carries no variant selector and imports no getenv."""
+    path = _lib.LIB_PATH
+    data = open(path, "rb").read()
+    for key in (b"FA_FWD_VARIANT", b"FA_BWD_VARIANT", b"FA_FWD_ABL"):
+        assert key not in data
+    import subprocess
+    nm = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True)
+    if nm.returncode == 0:
+        assert "getenv" not in nm.stdout
+
+
+def test_backward_rejects_mismatched_dtypes():
+    """flash_attention_backward.cc:51-154 types: q,k,v,o,m: T; l: float (Float16 ops) or T."""
+    import torch
+    t = lambda *s, dt=torch.float16: torch.zeros(s, dtype=dt)  # noqa: E731
+    Q, K, V, Oo, l, m, dO = (t(1, 8, 16), t(1, 8, 12), t(1, 8, 12), t(1, 8, 16), t(1, 16, dt=torch.float32),
+                             t(1, 16), t(1, 8, 16))
+    with pytest.raises(fa.InvalidArgumentError):  # all well-typed: only the device check fails on CPU
+        fa.attention_backward("full", 1, Q, K, V, Oo, l, m, dO, "none_front")
+    cases = {"K": dict(K=t(1, 8, 12, dt=torch.float32)), "V": dict(V=t(1, 8, 12, dt=torch.float32)),
+             "O": dict(O=t(1, 8, 16, dt=torch.float32)), "m": dict(m=t(1, 16, dt=torch.float32)),
+             "l": dict(l=t(1, 16))}
+    for name, over in cases.items():
+        args = dict(Q=Q, K=K, V=V, O=Oo, l=l, m=m, dO=dO)
+        args.update(over)
+        with pytest.raises(TypeError, match=name):
+            fa.attention_backward("full", 1, args["Q"], args["K"], args["V"], args["O"], args["l"], args["m"],
+                                  args["dO"], "none_front")
+    Q32 = [x.float() for x in (Q, K, V, Oo)]
+    with pytest.raises(TypeError, match="l must be"):  # fp32 op: l is T, not float16
+        fa.attention_backward("full", 1, *Q32, t(1, 16), t(1, 16, dt=torch.float32), dO.float(), "none_front")
+
+
 def test_backward_workspace_size():
     p = _prob("causal", [100], [60], b=3, d=16, vd=8, dtype=_lib.F16)
     n = _lib.lib().fa_backward_workspace_bytes(p)

@@ -127,5 +127,23 @@ def make_problem(dtype, policy, seq_dims, sync_mode, b, q_seq, k_seq, d, v_d,
     return p
 
 
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of the product sources, computed exactly as the Makefile's
+    SRC_HASH (csrc/*.hip, csrc/*.h, ../include/fa_api.h in make's byte-wise sort order)."""
+    import glob
+    import hashlib
+    rel = [os.path.relpath(p, _HERE) for p in glob.glob(os.path.join(_HERE, "csrc", "*.hip"))
+           + glob.glob(os.path.join(_HERE, "csrc", "*.h"))] + ["../include/fa_api.h"]
+    h = hashlib.sha256()
+    for r in sorted(rel, key=lambda x: x.encode()):
+        with open(os.path.join(_HERE, r), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build_info() -> str:
+    return lib().fa_build_info().decode()
+
+
 def last_error() -> str:
     return lib().fa_last_error().decode()

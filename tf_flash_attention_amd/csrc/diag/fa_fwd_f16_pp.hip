@@ -30,11 +30,10 @@
 // Numerics are those of fa_fwd_f16.hip / fa_fwd_f16_fast.hip (fp32 accumulation,
 // log2-domain lazy rebase with threshold 8, l relative to the stored fp16 m).
 // Replaces the reference's ForwardImpl (flash_attention.cu:425-1077) for these shapes.
-#include "fa_device.h"
-#include "fa_kernels.h"
-#include "fa_mfma.h"
+#include "../fa_device.h"
+#include "../fa_kernels.h"
+#include "../fa_mfma.h"
 
-#include <stdlib.h>
 
 namespace fa {
 namespace {
@@ -495,8 +494,7 @@ bool fwd_f16_pp_supported(const FwdArgs& a) {
 hipError_t launch_fwd_f16_pp(const FwdArgs& a, hipStream_t s) {
   const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
   auto kern = a.rule.policy == 0 ? fwd_f16_pp_kernel<0> : fwd_f16_pp_kernel<1>;
-  const char* ev = getenv("FA_FWD_VARIANT");
-  switch (ev ? atoi(ev) - 2100 : -1) {  // ablations, full policy only (timing diagnostics)
+  switch (diag_variant("FA_FWD_VARIANT") - 2100) {  // ablations, full policy only (timing diagnostics)
     case 1: kern = fwd_f16_pp_kernel<0, 1>; break;
     case 2: kern = fwd_f16_pp_kernel<0, 2>; break;
     case 3: kern = fwd_f16_pp_kernel<0, 3>; break;
@@ -514,7 +512,7 @@ hipError_t launch_fwd_f16_pp(const FwdArgs& a, hipStream_t s) {
     default: break;
   }
   hipError_t e =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
+      set_smem_once(reinterpret_cast<const void*>(kern), kSmem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kNW * 64), kSmem, s, a);
   return hipGetLastError();

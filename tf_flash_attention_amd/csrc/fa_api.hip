@@ -14,11 +14,46 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <mutex>
+#include <shared_mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/fa_api.h"
+#include "fa_device.h"
 #include "fa_kernels.h"
 #include "fa_rules.h"
+
+namespace fa {
+
+// (kernel, device) pairs whose dynamic-LDS limit is already raised.  Readers take the shared
+// lock; the first launch of a kernel on a device takes the exclusive one.  Replaces the
+// reference's per-launch cudaFuncSetAttribute (flash_attention.cu:2269, which sits inside an
+// assert and vanishes under NDEBUG — SURVEY N7).
+hipError_t set_smem_once(const void* kern, int bytes) {
+  struct Entry {
+    const void* kern;
+    int dev, bytes;
+  };
+  static std::shared_mutex mu;
+  static std::vector<Entry> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  {
+    std::shared_lock<std::shared_mutex> rd(mu);
+    for (const Entry& x : done)
+      if (x.kern == kern && x.dev == dev && x.bytes >= bytes) return hipSuccess;
+  }
+  std::unique_lock<std::shared_mutex> wr(mu);
+  for (const Entry& x : done)
+    if (x.kern == kern && x.dev == dev && x.bytes >= bytes) return hipSuccess;
+  e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.push_back({kern, dev, bytes});
+  return e;
+}
+
+}  // namespace fa
 
 namespace {
 
@@ -297,8 +332,17 @@ const char* fa_error_string(int status) {
 
 const char* fa_last_error(void) { return g_last_error.c_str(); }
 
+#ifndef FA_SRC_HASH
+#define FA_SRC_HASH "unknown"
+#endif
+#ifdef FA_DIAG
+#define FA_LIB_KIND "diagnostic (FA_DIAG: environment-selected variants)"
+#else
+#define FA_LIB_KIND "product"
+#endif
+
 const char* fa_build_info(void) {
-  return "tf_flash_attention_amd: gfx950; fwd={mfma_f16, mfma_f32, mfma_f64, generic(f16,f32,f64)}; bwd={mfma_f16 (two-pass / single-pass), mfma_f32 (two-pass), mfma_f64 (two-pass, d<=64), generic(f16,f32,f64)}";
+  return "tf_flash_attention_amd: src=" FA_SRC_HASH "; lib=" FA_LIB_KIND "; gfx950; fwd={mfma_f16, mfma_f32, mfma_f64, generic(f16,f32,f64)}; bwd={mfma_f16 (two-pass / single-pass), mfma_f32 (two-pass), mfma_f64 (two-pass, d<=64), generic(f16,f32,f64)}";
 }
 
 }  // extern "C"

@@ -343,8 +343,7 @@ hipError_t launch_main(const BwdArgs& a, hipStream_t s) {
   const int64_t nkb = (a.rule.k.n + kBK - 1) / kBK;
   const int smem = BSmem<D>::kTotal;
   auto kern = a.rule.policy == 0 ? bwd_f16_kernel<D, 0> : bwd_f16_kernel<D, 1>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     smem);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), smem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(kThreads), smem, s, a);
   return hipGetLastError();
@@ -358,10 +357,14 @@ bool bwd_f16_supported(const BwdArgs& a) {
 }
 
 hipError_t launch_bwd_f16(const BwdArgs& a, hipStream_t s) {
-  // FA_BWD_VARIANT=0 pins this single-pass atomic kernel (A/B runs); otherwise the two-pass
-  // kernels take the shapes they support
-  const char* ev = getenv("FA_BWD_VARIANT");
-  if (!(ev && atoi(ev) == 0) && bwd_f16_fast_supported(a)) return launch_bwd_f16_fast(a, s);
+  // the two-pass kernels take the shapes they support (diagnostic library: FA_BWD_VARIANT=0 pins
+  // this single-pass atomic kernel for A/B runs)
+#ifdef FA_DIAG
+  const bool pinned = diag_variant("FA_BWD_VARIANT") == 0;
+#else
+  constexpr bool pinned = false;
+#endif
+  if (!pinned && bwd_f16_fast_supported(a)) return launch_bwd_f16_fast(a, s);
   const int nq = a.rule.q.n;
   hipError_t e = hipMemsetAsync(a.ws_dQ, 0, sizeof(float) * (size_t)a.b * a.d * nq, s);
   if (e != hipSuccess) return e;

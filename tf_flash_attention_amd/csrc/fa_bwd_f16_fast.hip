@@ -755,8 +755,7 @@ hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
   using S = DkdvSmem<D, NW, PIPE ? 3 : 2>;
   const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
   auto kern = a.rule.policy == 0 ? bwd_dkdv_kernel<D, NW, WPE, 0, PIPE, ABL> : bwd_dkdv_kernel<D, NW, WPE, 1, PIPE, ABL>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     S::kTotal);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(NW * 64), S::kTotal, s, a);
   return hipGetLastError();
@@ -767,16 +766,10 @@ hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
   using S = DqSmem<D, NW>;
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
   auto kern = a.rule.policy == 0 ? bwd_dq_kernel<D, NW, WPE, 0, PRE> : bwd_dq_kernel<D, NW, WPE, 1, PRE>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     S::kTotal);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(NW * 64), S::kTotal, s, a);
   return hipGetLastError();
-}
-
-int bwd_variant() {
-  const char* e = getenv("FA_BWD_VARIANT");
-  return e ? atoi(e) : -1;
 }
 
 }  // namespace
@@ -796,8 +789,11 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(bwd_prep_kernel, dim3((unsigned)((nrows + kThrPrep - 1) / kThrPrep)), dim3(kThrPrep), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int v = bwd_variant();
-  if (max(a.d, a.v_d) <= 64) {
+#ifdef FA_DIAG
+  // FA_BWD_VARIANT selects A/B structures (82, 1067-1069, 1200, 1264, 1267, 1281) and the
+  // d = 128 dK/dV ablations 1301-1363 (outputs WRONG)
+  const int v = diag_variant("FA_BWD_VARIANT");
+  if (max(a.d, a.v_d) <= 64 && v >= 0) {
     switch (v) {
       case 82: e = launch_dkdv<64, 8, 2>(a, s); break;
       case 1067: case 1069: e = launch_dkdv<64, 4, 2, false, 64>(a, s); break;
@@ -810,24 +806,35 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
       default: return launch_dq<64, 4, 2>(a, s);
     }
   }
-  switch (v) {
-    case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
-    case 1200: e = launch_dkdv<128, 4, 1>(a, s); break;  // operand reads not run ahead (before the default)
-    case 1264: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
-    case 1267: e = launch_dkdv<128, 4, 1, false, 64 | 128>(a, s); break;
-    case 1301: e = launch_dkdv<128, 4, 1, false, 1>(a, s); break;
-    case 1302: e = launch_dkdv<128, 4, 1, false, 2>(a, s); break;
-    case 1304: e = launch_dkdv<128, 4, 1, false, 4>(a, s); break;
-    case 1308: e = launch_dkdv<128, 4, 1, false, 8>(a, s); break;
-    case 1316: e = launch_dkdv<128, 4, 1, false, 16>(a, s); break;
-    case 1324: e = launch_dkdv<128, 4, 1, false, 24>(a, s); break;
-    case 1338: e = launch_dkdv<128, 4, 1, false, 38>(a, s); break;
-    case 1363: e = launch_dkdv<128, 4, 1, false, 63>(a, s); break;
-    // tuned (c3): operand reads two MFMA pairs ahead in both passes (10.97 -> 9.93 ms backward)
-    default: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
+  if (max(a.d, a.v_d) > 64 && v >= 0) {
+    switch (v) {
+      case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
+      case 1200: e = launch_dkdv<128, 4, 1>(a, s); break;  // operand reads not run ahead (before the default)
+      case 1264: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
+      case 1267: e = launch_dkdv<128, 4, 1, false, 64 | 128>(a, s); break;
+      case 1301: e = launch_dkdv<128, 4, 1, false, 1>(a, s); break;
+      case 1302: e = launch_dkdv<128, 4, 1, false, 2>(a, s); break;
+      case 1304: e = launch_dkdv<128, 4, 1, false, 4>(a, s); break;
+      case 1308: e = launch_dkdv<128, 4, 1, false, 8>(a, s); break;
+      case 1316: e = launch_dkdv<128, 4, 1, false, 16>(a, s); break;
+      case 1324: e = launch_dkdv<128, 4, 1, false, 24>(a, s); break;
+      case 1338: e = launch_dkdv<128, 4, 1, false, 38>(a, s); break;
+      case 1363: e = launch_dkdv<128, 4, 1, false, 63>(a, s); break;
+      default: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
+    }
+    if (e != hipSuccess) return e;
+    if (v == 1200 || v == 1264) return launch_dq<128, 4, 1>(a, s);
+    return launch_dq<128, 4, 1, true>(a, s);
   }
+#endif
+  if (max(a.d, a.v_d) <= 64) {
+    e = launch_dkdv<64, 4, 2>(a, s);
+    if (e != hipSuccess) return e;
+    return launch_dq<64, 4, 2>(a, s);
+  }
+  // tuned (c3): operand reads two MFMA pairs ahead in both passes (10.97 -> 9.93 ms backward)
+  e = launch_dkdv<128, 4, 1, false, 64>(a, s);
   if (e != hipSuccess) return e;
-  if (v == 1200 || v == 1264) return launch_dq<128, 4, 1>(a, s);
   return launch_dq<128, 4, 1, true>(a, s);
 }
 

@@ -404,9 +404,9 @@ hipError_t launch_t(const BwdArgs& a, hipStream_t s) {
   auto kk = pol == 0 ? bwd_dkdv_f32_kernel<D, 0> : (pol == 1 ? bwd_dkdv_f32_kernel<D, 1> : bwd_dkdv_f32_kernel<D, 2>);
   auto kq = pol == 0 ? bwd_dq_f32_kernel<D, 0> : (pol == 1 ? bwd_dq_f32_kernel<D, 1> : bwd_dq_f32_kernel<D, 2>);
   constexpr int smk = dkdv32_smem<D>(), smq = dq32_smem<D>();
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kk), hipFuncAttributeMaxDynamicSharedMemorySize, smk);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kk), smk);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute(reinterpret_cast<const void*>(kq), hipFuncAttributeMaxDynamicSharedMemorySize, smq);
+  e = set_smem_once(reinterpret_cast<const void*>(kq), smq);
   if (e != hipSuccess) return e;
   const int64_t nkb = (a.rule.k.n + 127) / 128, nqb = (a.rule.q.n + 127) / 128;
   hipLaunchKernelGGL(kk, dim3((unsigned)(a.b * nkb)), dim3(kThr), smk, s, a);

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "fa_rules.h"
 
@@ -52,6 +53,20 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
   const uint32_t q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
+
+// host: hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device), thread-safe
+// (fa_api.hip); later launches of the same kernel on the same device skip the runtime call
+hipError_t set_smem_once(const void* kern, int bytes);
+
+#ifdef FA_DIAG
+// host, diagnostic library only (libfa_hip_diag.so, built with -DFA_DIAG for tools/): A/B and
+// ablation variants are selected from the environment.  The product library has no variant code
+// and reads no environment variable.
+inline int diag_variant(const char* name) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : -1;
+}
+#endif
 
 }  // namespace fa
 

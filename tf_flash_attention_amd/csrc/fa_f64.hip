@@ -582,8 +582,7 @@ hipError_t launch_fwd_t(const FwdArgs& a, hipStream_t s) {
   constexpr int smem = 8 * (sm1 > sm2 ? sm1 : sm2);
   const int pol = policy_class(a.rule);
   auto kern = pol == 0 ? fwd_f64_kernel<D, 0> : (pol == 1 ? fwd_f64_kernel<D, 1> : fwd_f64_kernel<D, 2>);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     smem);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), smem);
   if (e != hipSuccess) return e;
   const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kThr), smem, s, a);
@@ -596,9 +595,9 @@ hipError_t launch_bwd_t(const BwdArgs& a, hipStream_t s) {
   auto kk = pol == 0 ? bwd_dkdv_f64_kernel<D, 0> : (pol == 1 ? bwd_dkdv_f64_kernel<D, 1> : bwd_dkdv_f64_kernel<D, 2>);
   auto kq = pol == 0 ? bwd_dq_f64_kernel<D, 0> : (pol == 1 ? bwd_dq_f64_kernel<D, 1> : bwd_dq_f64_kernel<D, 2>);
   constexpr int smem = bwd64_smem<D>();
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kk), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kk), smem);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute(reinterpret_cast<const void*>(kq), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  e = set_smem_once(reinterpret_cast<const void*>(kq), smem);
   if (e != hipSuccess) return e;
   const int64_t nkb = (a.rule.k.n + kBM - 1) / kBM, nqb = (a.rule.q.n + kBM - 1) / kBM;
   hipLaunchKernelGGL(kk, dim3((unsigned)(a.b * nkb)), dim3(kThr), smem, s, a);

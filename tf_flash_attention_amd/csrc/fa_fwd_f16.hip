@@ -457,18 +457,10 @@ hipError_t launch_t(const FwdArgs& a, hipStream_t s) {
   auto kern = pol == 0 ? (fast ? fwd_f16_kernel<D, NW, 0, true, F> : fwd_f16_kernel<D, NW, 0, false, F>)
             : pol == 1 ? (fast ? fwd_f16_kernel<D, NW, 1, true, F> : fwd_f16_kernel<D, NW, 1, false, F>)
                        : (fast ? fwd_f16_kernel<D, NW, 2, true, F> : fwd_f16_kernel<D, NW, 2, false, F>);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     smem);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), smem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(NW * 64), smem, s, a);
   return hipGetLastError();
-}
-
-// FA_FWD_VARIANT (env, read per call) selects a structure for A/B timing runs
-// in one process: <NW><F>, e.g. "41" = 4 waves, flags 1.  Unset -> tuned default.
-int env_variant() {
-  const char* e = getenv("FA_FWD_VARIANT");
-  return e ? atoi(e) : -1;
 }
 
 }  // namespace
@@ -479,11 +471,10 @@ bool fwd_f16_supported(const FwdArgs& a) {
 
 hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s) {
   const int dm = max(a.d, a.v_d);
-  const int v = env_variant();
-  // FA_FWD_VARIANT < 1000 pins the general kernel (A/B runs); otherwise the streamlined one takes its shapes
-  if ((v < 0 || v >= 1000) && fwd_f16_fast_supported(a)) return launch_fwd_f16_fast(a, s);
-  if (dm <= 32) return launch_t<32, 4, 8>(a, s);
-  if (dm <= 64) {
+#ifdef FA_DIAG
+  // FA_FWD_VARIANT = <NW><F> below 1000 pins this general kernel (A/B runs), e.g. 408
+  const int v = diag_variant("FA_FWD_VARIANT");
+  if (v >= 0 && v < 1000 && dm > 32 && dm <= 64) {
     switch (v) {
       case 400: return launch_t<64, 4, 0>(a, s);
       case 408: return launch_t<64, 4, 8>(a, s);
@@ -492,12 +483,20 @@ hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s) {
       case 800: return launch_t<64, 8, 0>(a, s);
       case 808: return launch_t<64, 8, 8>(a, s);
       case 840: return launch_t<64, 8, 40>(a, s);
-      default:
-        // local bands: ~10 key tiles per block, so block prologue/epilogue matter;
-        // 4-wave blocks let two blocks per CU cover each other's (c4: 5.2 vs 5.9 ms)
-        if (a.rule.policy == 2) return launch_t<64, 4, 8>(a, s);
-        return launch_t<64, 8, 8>(a, s);
+      default: break;
     }
+  }
+  const bool pinned = v >= 0 && v < 1000;
+#else
+  constexpr bool pinned = false;
+#endif
+  if (!pinned && fwd_f16_fast_supported(a)) return launch_fwd_f16_fast(a, s);
+  if (dm <= 32) return launch_t<32, 4, 8>(a, s);
+  if (dm <= 64) {
+    // local bands: ~10 key tiles per block, so block prologue/epilogue matter;
+    // 4-wave blocks let two blocks per CU cover each other's (c4: 5.2 vs 5.9 ms)
+    if (a.rule.policy == 2) return launch_t<64, 4, 8>(a, s);
+    return launch_t<64, 8, 8>(a, s);
   }
   return launch_t<128, 4, 8>(a, s);
 }

@@ -490,16 +490,10 @@ hipError_t launch_fast_t(const FwdArgs& a, hipStream_t s) {
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
   const int smem = S::kTotal;
   auto kern = a.rule.policy == 0 ? fwd_f16_fast_kernel<D, NW, 0, F> : fwd_f16_fast_kernel<D, NW, 1, F>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     smem);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), smem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(NW * 64), smem, s, a);
   return hipGetLastError();
-}
-
-int fast_variant() {
-  const char* e = getenv("FA_FWD_VARIANT");
-  return e ? atoi(e) : -1;
 }
 
 }  // namespace
@@ -514,24 +508,16 @@ bool fwd_f16_fast_supported(const FwdArgs& a) {
 }
 
 hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
-  // FA_FWD_VARIANT = 1<NW><F>: e.g. 186 = 8 waves, flags 6 (timing runs); unset -> tuned default
-  const int v = fast_variant();
   const bool d64 = max(a.d, a.v_d) <= 64;
-  // paired-block kernel (one wave per SIMD): FA_FWD_VARIANT=2000 selects it for every rule it takes
+#ifdef FA_DIAG
+  // FA_FWD_VARIANT = 1<NW><F>: e.g. 186 = 8 waves, flags 6; 20xx the paired-block kernel, 22xx /
+  // 23xx the ping-pong kernels for every rule they take; 1899 + FA_FWD_ABL ablations (outputs WRONG)
+  const int v = diag_variant("FA_FWD_VARIANT");
   if (fwd_f16_pp_supported(a) && v >= 2000 && v < 2200) return launch_fwd_f16_pp(a, s);
-  // ping-pong kernel (two wave groups alternating MFMA / softmax phases): the default for
-  // d <= 64 under the full policy (c2: 948 vs 904 TF/s for the 8-wave kernel below);
-  // FA_FWD_VARIANT=22xx forces it (and its variants) for every rule it takes
-  if (fwd_f16_pingpong_supported(a) && ((v < 0 && a.rule.policy == 0) || (v >= 2200 && v < 2300)))
-    return launch_fwd_f16_pingpong(a, s);
-  // d in (64, 128]: the ping-pong kernel is the default for the full and causal policies (c3
-  // forward: 2.52 vs 3.16 ms for the 4-wave kernel below); local windows keep the 4-wave blocks
-  // (short rule-bounded rows); FA_FWD_VARIANT=23xx forces it for every rule it takes
-  if (fwd_f16_pingpong128_supported(a) && ((v < 0 && a.rule.policy != 2) || (v >= 2300 && v < 2400)))
-    return launch_fwd_f16_pingpong128(a, s);
-  if (d64 && v == 1899) {  // ablations (timing only)
-    const char* e = getenv("FA_FWD_ABL");
-    switch (e ? atoi(e) : 0) {
+  if (fwd_f16_pingpong_supported(a) && v >= 2200 && v < 2300) return launch_fwd_f16_pingpong(a, s);
+  if (fwd_f16_pingpong128_supported(a) && v >= 2300 && v < 2400) return launch_fwd_f16_pingpong128(a, s);
+  if (d64 && v == 1899) {
+    switch (diag_variant("FA_FWD_ABL")) {
       case 64: return launch_fast_t<64, 8, 6 | 64>(a, s);
       case 128: return launch_fast_t<64, 8, 6 | 128>(a, s);
       case 256: return launch_fast_t<64, 8, 6 | 256>(a, s);
@@ -554,20 +540,34 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
       case 144: return launch_fast_t<64, 4, 4>(a, s);
       case 1414: return launch_fast_t<64, 4, 14>(a, s);
       case 1412: return launch_fast_t<64, 4, 12>(a, s);
-      default:
-        // tuned on MI355X: full-length key loops (c2) 8 waves x 32 queries, two key tiles per
-        // barrier; rule-bounded short loops (local windows, c4) 4-wave blocks with one tile per
-        // barrier (48 KB of LDS) so two blocks per CU cover each other's prologue / epilogue
-        if (a.rule.policy == 2) return launch_fast_t<64, 4, kFPrio | kFLateV>(a, s);
-        return launch_fast_t<64, 8, kFPrio | kFLateV | kFTpb2>(a, s);
+      default: break;
+    }
+  } else {
+    switch (v) {
+      case 140: return launch_fast_t<128, 4, 0>(a, s);
+      case 146: return launch_fast_t<128, 4, 6>(a, s);
+      default: break;
     }
   }
-  switch (v) {
-    case 140: return launch_fast_t<128, 4, 0>(a, s);
-    case 146: return launch_fast_t<128, 4, 6>(a, s);
-    // tuned (c3 forward, MI355X): 4 waves (one per SIMD), static priority, late V reads
-    default: return launch_fast_t<128, 4, kFPrio | kFLateV>(a, s);
+  const bool tuned = v < 0;
+#else
+  constexpr bool tuned = true;
+#endif
+  // ping-pong kernel (two wave groups alternating MFMA / softmax phases): the default for
+  // d <= 64 under the full policy (c2: 948 vs 904 TF/s for the 8-wave kernel below)
+  if (tuned && a.rule.policy == 0 && fwd_f16_pingpong_supported(a)) return launch_fwd_f16_pingpong(a, s);
+  // d in (64, 128]: the ping-pong kernel is the default for the full and causal policies (c3
+  // forward: 2.52 vs 3.16 ms for the 4-wave kernel below); local windows keep the 4-wave blocks
+  if (tuned && a.rule.policy != 2 && fwd_f16_pingpong128_supported(a)) return launch_fwd_f16_pingpong128(a, s);
+  if (d64) {
+    // tuned on MI355X: full-length key loops 8 waves x 32 queries, two key tiles per barrier;
+    // rule-bounded short loops (local windows, c4) 4-wave blocks with one tile per barrier
+    // (48 KB of LDS) so two blocks per CU cover each other's prologue / epilogue
+    if (a.rule.policy == 2) return launch_fast_t<64, 4, kFPrio | kFLateV>(a, s);
+    return launch_fast_t<64, 8, kFPrio | kFLateV | kFTpb2>(a, s);
   }
+  // tuned (c3 forward, MI355X): 4 waves (one per SIMD), static priority, late V reads
+  return launch_fast_t<128, 4, kFPrio | kFLateV>(a, s);
 }
 
 }  // namespace fa

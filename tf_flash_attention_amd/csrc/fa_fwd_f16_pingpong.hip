@@ -33,8 +33,6 @@
 #include "fa_kernels.h"
 #include "fa_mfma.h"
 
-#include <stdlib.h>
-
 namespace fa {
 namespace {
 
@@ -611,7 +609,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     const uint32_t vals[10] = {(uint32_t)wg_t0, (uint32_t)(wg_t0 >> 32), (uint32_t)(wg_t1 - wg_t0), (uint32_t)(wg_t2 - wg_t0),
                                (uint32_t)(t3 - wg_t0), (uint32_t)(wg_c1 - wg_c0), (uint32_t)(wg_c2 - wg_c0),
                                (uint32_t)(c3 - wg_c0), hw, xcc};
-    if (w == 0 && lane < 10) {
+    if (w == 0 && lane < 10 && q0 + lane < nq) {
       uint32_t v = 0;
 #pragma unroll
       for (int k = 0; k < 10; ++k) v = (lane == k) ? vals[k] : v;
@@ -619,7 +617,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     }
   }
   if constexpr ((F & kFStamp) != 0) {  // diagnostic build: stamps over this wave's first l entries
-    if (lane < 6) {
+    if (lane < 6 && wq0 + lane < nq) {
       uint64_t v = 0;
 #pragma unroll
       for (int k = 0; k < 6; ++k) v = (lane == k) ? st_acc[k] : v;
@@ -634,7 +632,7 @@ hipError_t launch_t(const FwdArgs& a, hipStream_t s) {
   auto kern = a.rule.policy == 0 ? fwd_f16_pingpong_kernel<0, F> : fwd_f16_pingpong_kernel<1, F>;
   constexpr int smem = Ring<(F & kFDma) != 0>::kSmem;
   hipError_t e =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+      set_smem_once(reinterpret_cast<const void*>(kern), smem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kNW * 64), smem, s, a);
   return hipGetLastError();
@@ -651,9 +649,13 @@ bool fwd_f16_pingpong_supported(const FwdArgs& a) {
          rule_is_interval(a.rule) && a.b * ((a.rule.q.n + kBM - 1) / kBM) < (1ll << 31);
 }
 
+// tuned (c2, MI355X): MFMA phases at priority 1, fragment reads and staging interleaved with
+// the MFMAs (full policy; 0.5526-0.5716 ms against 0.595 for 2206)
+constexpr int kFDefault = kFPrio | kFStoresLate | kFInterleave | kFIlvStores;
+
 hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
-  const char* ev = getenv("FA_FWD_VARIANT");
-  switch (ev ? atoi(ev) : -1) {
+#ifdef FA_DIAG
+  switch (diag_variant("FA_FWD_VARIANT")) {
     case 2200: return launch_t<0>(a, s);
     case 2203: return launch_t<kFPrio | kFStamp>(a, s);
     case 2204: return launch_t<kFPrio | kFStampWG>(a, s);
@@ -686,10 +688,10 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2267: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag>(a, s);
     case 2268: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
     case 2201: return launch_t<kFPrio>(a, s);
-    // tuned (c2, MI355X): MFMA phases at priority 1, fragment reads and staging interleaved with
-    // the MFMAs (full policy; 0.5526-0.5716 ms against 0.595 for 2206)
-    default: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores>(a, s);
+    default: break;
   }
+#endif
+  return launch_t<kFDefault>(a, s);
 }
 
 }  // namespace fa

@@ -396,7 +396,7 @@ hipError_t launch_t(const FwdArgs& a, hipStream_t s) {
   const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
   auto kern = a.rule.policy == 0 ? fwd_f16_pingpong128_kernel<0, F> : fwd_f16_pingpong128_kernel<1, F>;
   hipError_t e =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
+      set_smem_once(reinterpret_cast<const void*>(kern), kSmem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kNW * 64), kSmem, s, a);
   return hipGetLastError();
@@ -413,11 +413,10 @@ bool fwd_f16_pingpong128_supported(const FwdArgs& a) {
 }
 
 hipError_t launch_fwd_f16_pingpong128(const FwdArgs& a, hipStream_t s) {
-  const char* ev = getenv("FA_FWD_VARIANT");
-  switch (ev ? atoi(ev) : -1) {
-    case 2300: return launch_t<0>(a, s);
-    default: return launch_t<kFPrio>(a, s);
-  }
+#ifdef FA_DIAG
+  if (diag_variant("FA_FWD_VARIANT") == 2300) return launch_t<0>(a, s);
+#endif
+  return launch_t<kFPrio>(a, s);
 }
 
 }  // namespace fa

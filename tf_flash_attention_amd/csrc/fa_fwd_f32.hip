@@ -285,8 +285,7 @@ hipError_t launch_t(const FwdArgs& a, hipStream_t s) {
   const int smem = Smem32<D>::kTotal;
   const int pol = a.rule.policy == 0 ? 0 : (rule_is_interval(a.rule) ? 1 : 2);
   auto kern = pol == 0 ? fwd_f32_kernel<D, 0> : (pol == 1 ? fwd_f32_kernel<D, 1> : fwd_f32_kernel<D, 2>);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     smem);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), smem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kThreads), smem, s, a);
   return hipGetLastError();

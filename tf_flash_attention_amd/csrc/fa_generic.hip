@@ -296,7 +296,7 @@ hipError_t launch_fwd_generic_t(const FwdArgs& a, hipStream_t stream) {
   const int64_t nqb = (nq + kGBQ - 1) / kGBQ;
   const size_t smem = sizeof(A) * ((size_t)a.d * kGBQ + (size_t)a.d * kGBK + (size_t)a.v_d * kGBK + kGBQ * (kGBK + 1));
   auto kern = fwd_generic_kernel<T, MAXD>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), (int)smem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kThreads), smem, stream, a);
   return hipGetLastError();
@@ -315,7 +315,7 @@ hipError_t launch_bwd_generic_t(const BwdArgs& a, hipStream_t stream) {
   const int64_t nkb = (nk + kGBK - 1) / kGBK;
   const size_t smem = sizeof(A) * ((size_t)(a.d + a.v_d) * kGBK + (size_t)(a.d + a.v_d) * kGBQ + 2 * kGBQ * (kGBK + 1) + 2 * kGBQ);
   auto kern = bwd_generic_kernel<T, MAXD>;
-  e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  e = set_smem_once(reinterpret_cast<const void*>(kern), (int)smem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(kThreads), smem, stream, a);
   e = hipGetLastError();

@@ -88,6 +88,11 @@ FA_HD bool check_orders_bf(const Rule& r, int32_t qo, int32_t ko) {
 
 FA_HD int32_t imin32(int32_t a, int32_t b) { return a < b ? a : b; }
 FA_HD int32_t imax32(int32_t a, int32_t b) { return a > b ? a : b; }
+// a + b for a >= 0, b >= 0, saturated at INT32_MAX (orders are < 2^30, windows up to INT32_MAX)
+FA_HD int32_t sat_add32(int32_t a, int32_t b) {
+  const int64_t s = (int64_t)a + (int64_t)b;
+  return s > 0x7fffffff ? 0x7fffffff : (int32_t)s;
+}
 
 // Window bounding box in ORDER space for a block of partners whose orders span
 // [omin, omax] (LocalAttentionPolicy::IsSkipped, flash_attention.h:100-115).
@@ -97,22 +102,26 @@ FA_HD int32_t imax32(int32_t a, int32_t b) { return a > b ? a : b; }
 FA_HD void local_order_bounds(const Rule& r, int32_t omin, int32_t omax,
                               int32_t lo_reach, int32_t hi_reach,
                               int32_t* lo, int32_t* hi) {
+  // a reach past the grid extent R clamps like R itself; clamping first keeps c + reach inside
+  // int32 for windows up to INT32_MAX (validated: ws << ls <= INT32_MAX)
+  const int32_t lr0 = imin32(lo_reach, r.R0), hr0 = imin32(hi_reach, r.R0);
+  const int32_t lr1 = imin32(lo_reach, r.R1), hr1 = imin32(hi_reach, r.R1);
   const int32_t c0min = omin & (r.R0 - 1), c0max = omax & (r.R0 - 1);
-  int32_t l0 = imax32(c0min - lo_reach, 0);
-  int32_t h0 = imin32(c0max + hi_reach, r.R0 - 1);
+  int32_t l0 = imax32(c0min - lr0, 0);
+  int32_t h0 = imin32(c0max + hr0, r.R0 - 1);
   if (r.seq_dims == 1) {
     *lo = l0; *hi = h0; return;
   }
   const int32_t c1min = (omin >> r.log2R0) & (r.R1 - 1), c1max = (omax >> r.log2R0) & (r.R1 - 1);
-  const int32_t l1 = imax32(c1min - lo_reach, 0);
-  const int32_t h1 = imin32(c1max + hi_reach, r.R1 - 1);
+  const int32_t l1 = imax32(c1min - lr1, 0);
+  const int32_t h1 = imin32(c1max + hr1, r.R1 - 1);
   // When the row bound is clamped at the grid edge, partners of EARLIER/LATER
   // block rows can reach any column of the clamped row: widen dim 0 there.
   // (The reference's IsSkipped keeps the unclamped column bound and can skip
   // a tile holding allowed pairs in that corner case; the vanilla test oracle
   // — our parity target — attends them.)
-  if (c1min - lo_reach < 0) l0 = 0;
-  if (c1max + hi_reach > r.R1 - 1) h0 = r.R0 - 1;
+  if (c1min - lr1 < 0) l0 = 0;
+  if (c1max + hr1 > r.R1 - 1) h0 = r.R0 - 1;
   *lo = l0 + (l1 << r.log2R0);
   *hi = h0 + (h1 << r.log2R0);
 }
@@ -175,10 +184,10 @@ FA_HD void key_interval(const Rule& r, int32_t qi, int32_t* klo, int32_t* khi) {
   int32_t ohi = qo;  // causal: ko <= qo
   *klo = 0;
   if (r.policy == 2) {  // 1d: coordinate == order; |qo - ko| <= ws - 1
-    if (r.look_ahead != 1) ohi = qo + (r.ws - 1);
+    if (r.look_ahead != 1) ohi = sat_add32(qo, r.ws - 1);
     *klo = lower_bound_order(r.k, r, qo - (r.ws - 1));
   }
-  *khi = lower_bound_order(r.k, r, ohi + 1) - 1;
+  *khi = lower_bound_order(r.k, r, sat_add32(ohi, 1)) - 1;
 }
 
 // Inclusive query-index interval [*qlo, *qhi] allowed for key index ki under an
@@ -192,7 +201,7 @@ FA_HD void query_interval(const Rule& r, int32_t ki, int32_t* qlo, int32_t* qhi)
   *qhi = nq - 1;
   if (r.policy == 2) {  // 1d: |qo - ko| <= ws - 1
     if (r.look_ahead != 1) *qlo = lower_bound_order(r.q, r, ko - (r.ws - 1));
-    *qhi = lower_bound_order(r.q, r, ko + r.ws) - 1;
+    *qhi = lower_bound_order(r.q, r, sat_add32(ko, r.ws)) - 1;
   }
 }
 

@@ -205,6 +205,14 @@ def attention_backward(policy: str, seq_dims: int, Q, K, V, O, l, m, dO, sync_mo
     if float16_op is None:
         float16_op = Q.dtype == torch.float16
     dt = _dtype_id(Q, float16_op)
+    # the typed op inputs of flash_attention_backward.cc:51-154: q, k, v, o, m: T; l: float for the
+    # Float16 ops, T otherwise (a mismatched l would be read at the wrong width)
+    for name, t in (("K", K), ("V", V), ("O", O), ("m", m)):
+        if t.dtype != Q.dtype:
+            raise TypeError(f"{name} must have Q's dtype {Q.dtype}, got {t.dtype}")
+    l_dtype = torch.float32 if dt == _lib.F16 else Q.dtype
+    if l.dtype != l_dtype:
+        raise TypeError(f"l must be {l_dtype} for this op, got {l.dtype}")
     _check_device_tensors(Q, K, V, O, l, m, dO)
     Q, K, V, O, l, m, dO = (t.contiguous() for t in (Q, K, V, O, l, m, dO))
     dO = dO.to(Q.dtype)

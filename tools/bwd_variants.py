@@ -8,6 +8,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# variant / ablation / stamp builds live only in the diagnostic library (make -C tf_flash_attention_amd diag)
+os.environ.setdefault("FA_HIP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                               "tf_flash_attention_amd", "libfa_hip_diag.so"))
 from tf_flash_attention_amd import flash_attention as fa  # noqa: E402
 import bench  # noqa: E402
 

@@ -115,13 +115,27 @@ double max_rel_err(const std::vector<unsigned char>& got, int dt, const std::vec
 
 int check() {
   struct Case { int dt, pol, sd, mode; int qs[2], ks[2]; int d, ws, ls, causal; };
+  // every policy x dtype x seq_dims (the reference's registered op matrix,
+  // flash_attention_forward.cc:548-589), sync modes and ragged extents mixed in
   const Case cases[] = {
       {FA_F16, FA_FULL, 1, FA_NONE_FRONT, {256, 1}, {192, 1}, 64, 1, 0, 0},
       {FA_F16, FA_CAUSAL, 1, FA_NONE_FRONT, {320, 1}, {320, 1}, 128, 1, 0, 0},
       {FA_F16, FA_LOCAL, 1, FA_SCALE_END, {200, 1}, {264, 1}, 64, 33, 0, 1},
+      {FA_F16, FA_FULL, 2, FA_SCALE_FRONT, {12, 10}, {24, 20}, 64, 1, 0, 0},
+      {FA_F16, FA_CAUSAL, 2, FA_NONE_FRONT, {16, 9}, {16, 9}, 96, 1, 0, 0},
+      {FA_F16, FA_LOCAL, 2, FA_SCALE_FRONT, {10, 12}, {20, 24}, 64, 3, 1, 0},
+      {FA_F32, FA_FULL, 1, FA_SCALE_FRONT, {130, 1}, {260, 1}, 64, 1, 0, 0},
+      {FA_F32, FA_CAUSAL, 1, FA_SCALE_END, {150, 1}, {75, 1}, 128, 1, 0, 0},
+      {FA_F32, FA_LOCAL, 1, FA_NONE_FRONT, {300, 1}, {300, 1}, 32, 17, 1, 1},
       {FA_F32, FA_FULL, 2, FA_SCALE_FRONT, {8, 8}, {16, 16}, 64, 1, 0, 0},
+      {FA_F32, FA_CAUSAL, 2, FA_SCALE_END, {8, 12}, {16, 6}, 48, 1, 0, 0},
       {FA_F32, FA_LOCAL, 2, FA_NONE_FRONT, {9, 7}, {9, 7}, 32, 2, 1, 0},
+      {FA_F64, FA_FULL, 1, FA_NONE_FRONT, {100, 1}, {90, 1}, 64, 1, 0, 0},
       {FA_F64, FA_CAUSAL, 1, FA_SCALE_END, {77, 1}, {130, 1}, 16, 1, 0, 0},
+      {FA_F64, FA_LOCAL, 1, FA_SCALE_FRONT, {64, 1}, {128, 1}, 32, 9, 0, 0},
+      {FA_F64, FA_FULL, 2, FA_SCALE_END, {6, 6}, {12, 12}, 32, 1, 0, 0},
+      {FA_F64, FA_CAUSAL, 2, FA_NONE_FRONT, {7, 9}, {7, 9}, 64, 1, 0, 0},
+      {FA_F64, FA_LOCAL, 2, FA_NONE_FRONT, {8, 8}, {8, 8}, 16, 2, 0, 1},
   };
   int failures = 0;
   std::mt19937_64 rng(1234);
