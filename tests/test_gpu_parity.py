@@ -245,6 +245,23 @@ def test_local_band_mfma(dtype, ws, causal, mode, nq, nk):
     run_case(dtype, "local", 1, mode, (2,), 64, 64, (nq,), (nk,), ws, 0, causal, seed=ws)
 
 
+# the persistent band forward (fa_fwd_f16_band.hip: fp16 1d local, ls = 0, d <= 64 = v_d, nq % 8 == 0):
+# workgroups that walk several items across slice boundaries (more items than CUs), ragged last
+# blocks, nq != nk under the scale maps, causal windows, the smallest and widest windows it takes
+@pytest.mark.parametrize("batch,nq,nk,ws,causal,mode,d", [
+    ((5, 13), 1024, 1024, 96, False, "none_front", 64),
+    ((3, 40), 2048, 2048, 256, False, "none_front", 64),
+    ((7, 41), 1000, 1000, 1, False, "none_front", 64),
+    ((2, 150), 776, 1552, 130, True, "scale_front", 48),
+    ((300,), 1552, 520, 40, False, "scale_end", 64),
+    ((2, 131), 1024, 1024, 700, True, "none_front", 64),
+])
+def test_band_forward_persistent(batch, nq, nk, ws, causal, mode, d):
+    b = int(np.prod(batch))
+    run_case(np.float16, "local", 1, mode, batch, d, 64, (nq,), (nk,), ws, 0, causal, seed=ws + b,
+             slices=sorted({0, 1, b // 3, b // 2 + 1, b - 2, b - 1}))
+
+
 @pytest.mark.parametrize("d,vd", [(64, 32), (24, 64), (100, 100), (7, 3)])
 def test_odd_channels(d, vd):
     for dt in DTYPES:

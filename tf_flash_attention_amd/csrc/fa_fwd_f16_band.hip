@@ -1,0 +1,652 @@
+// fa_fwd_f16_band.hip — persistent fp16 forward for 1d local windows (a band of 2·ws-1 keys
+// around each query, unit stride), 32 < max(d, v_d) <= 64.  BASELINE config 4's shape.
+//
+// A band block touches few key tiles (ws = 256, 256 queries: 12 tiles), so a kernel that
+// launches one workgroup per query block spends a large share of its time starting and
+// ending blocks: loading Q, filling the K/V pipeline, storing O (round 1: c4 at 20 % MFMA
+// busy, 10 scalar instructions per MFMA).  Here one workgroup per CU walks a contiguous
+// list of blocks ("items": the query blocks of consecutive (batch, head) slices in order)
+// as ONE stream of key tiles:
+//
+//   * every item is exactly T tile positions (T = the most tiles any block's band spans,
+//     rounded up to a multiple of 4, >= 12); positions past an item's band load zeros and are
+//     skipped by every wave.  The item loop is unrolled over its T positions, so ring slots,
+//     staging sets and every per-position decision are compile-time;
+//   * the K/V staging (registers, loads five / four positions ahead, stored two positions
+//     later; LDS rings of four slots) runs straight across item boundaries;
+//   * the next item's Q image is loaded one 16-B chunk per thread at positions 2-5 and stored
+//     into the second of two LDS Q buffers at 4-7; each wave reads its new Q fragments in the
+//     VALU phase of the item's last position;
+//   * at position 0 of the next item the waves write the finished item's O (fp16, [c][256 q])
+//     over its dead Q buffer and its l / m beside it; at positions 2-3 whole 16-B rows leave
+//     for HBM (coalesced; the per-value stores of a per-block kernel touch 32-64 lines each);
+//   * every MFMA phase issues a fixed set of vector-memory operations, so hipcc's vmcnt waits
+//     stay exact (a conditional store anywhere in the stream made every staging store wait
+//     for the loads issued one phase earlier);
+//   * K / V fragments are read inside the MFMA phase that uses them, two k-steps ahead: the
+//     registers that would carry them across the VALU phase hold the stream's staging;
+//   * the running reference m_run carries over items: an item's first tile seeds it once
+//     (one exp pass), and its first PV / row sums start the accumulators (no reset).
+//
+// Inside an item the structure is the ping-pong of fa_fwd_f16_pingpong.hip (eight waves, two
+// groups alternating MFMA and softmax phases, unconditional MFMAs with P zeroed for a wave's
+// skipped tiles, fp32 accumulation, log2-domain lazy rebase at 8, row sums in running
+// accumulators, l relative to the stored fp16 m).  Replaces the reference's ForwardImpl
+// (flash_attention.cu:425-1077) under LocalAttentionPolicy (flash_attention.h:117-140) for
+// these shapes.
+#include "fa_device.h"
+#include "fa_kernels.h"
+#include "fa_mfma.h"
+
+#include <string.h>
+
+namespace fa {
+namespace {
+
+using namespace mf;
+
+constexpr int kD = 64;
+constexpr int kBN = 64;              // keys per tile
+constexpr int kNW = 8;               // waves per workgroup, two per SIMD
+constexpr int kBM = 32 * kNW;        // queries per item
+constexpr int kQRow = 2 * kBM;       // bytes per Q row in LDS
+constexpr int kQImg = kD * kQRow;    // 32 KB
+constexpr int kTile = kD * kBN * 2;  // 8 KB
+constexpr int kNS = 4;               // ring slots (K and V each)
+constexpr int kOffK = 2 * kQImg;     // two Q buffers first
+constexpr int kOffV = kOffK + kNS * kTile;
+constexpr int kOffLM = kOffV + kNS * kTile;   // l (fp32) and m (fp16) of a finished item: 1.5 KB
+constexpr int kOffTab = kOffLM + 6 * kBM;     // kt0 of every query block of a slice (int32)
+constexpr int kMaxTab = 4096;                 // query blocks per slice: nq <= 1M
+constexpr int kSmem = kOffTab + 4 * kMaxTab;  // 145.5 KB
+// Item timeline (positions it = 0 .. T-1 of item n+1): VALU(0) writes item n's O / l / m into
+// LDS (O over Q buffer n&1, dead by then); MFMA(2), MFMA(3) store it to HBM; MFMA(2..5) load
+// item n+2's Q chunks, MFMA(4..7) store them into buffer n&1 (after the O reads); VALU(T-1)
+// reads them as fragments: with T >= 12 a barrier separates every store from every read.
+constexpr int kMinT = 12;
+constexpr float kRescaleThr = 8.f;
+
+struct BandArgs {
+  FwdArgs a;
+  int64_t n_items;  // b * ceil(nq / kBM)
+  int32_t T;        // tile positions per item
+  int32_t n_wg;     // workgroups (persistent)
+};
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(IC<B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// wave-uniform description of one item
+struct Item {
+  int32_t sl;   // slice, relative to the workgroup's first slice
+  int32_t q0;   // first query (nq past the list: no wave active)
+  int32_t kt0;  // first key of its first tile (nk past the list: every load reads zeros)
+};
+
+// T (positions per item) is a template parameter, a multiple of 4: the item loop is unrolled over
+// its positions, so ring slots, staging sets and every "which position of the item" decision are
+// compile-time (no per-phase selects or dummy operations) and a position p = n*T + it has
+// p mod 4 == it mod 4
+template <int T, bool STAMP = false>
+__global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char_t* smem = (lds_char_t*)smem_raw;
+  const FwdArgs& a = ba.a;
+  constexpr float kNegInf = -__builtin_huge_valf();
+
+  const int nq = a.rule.q.n, nk = a.rule.k.n;
+  static_assert(T % 4 == 0 && T >= kMinT, "T: a multiple of 4, at least kMinT");
+  const int nqb = (nq + kBM - 1) / kBM;
+  // this workgroup's items [it_begin, it_end): contiguous, in (slice, block) order
+  const int64_t g = blockIdx.x;
+  const int64_t it_begin = g * ba.n_items / ba.n_wg, it_end = (g + 1) * ba.n_items / ba.n_wg;
+  const int n_local = (int)(it_end - it_begin);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, r = lane & 31;
+  const int gq = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const int d = a.d, vd = a.v_d;
+  const float c2 = (float)a.scale * kLog2e;
+
+  // one buffer descriptor per tensor over the workgroup's slices [sl0, sl0 + nsl): per-item
+  // offsets ride in soffset (host check: the span stays below 2^31 bytes, so offset 0x80000000
+  // still reads zeros)
+  const int64_t sl0 = it_begin / nqb;
+  const int nsl = (int)((it_end - 1) / nqb - sl0 + 1);
+  const uint32_t qsl = 2u * d * nq, ksl = 2u * d * nk, vsl = 2u * vd * nk;  // bytes per slice
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(static_cast<const __half*>(a.Q) + sl0 * (int64_t)d * nq, qsl * nsl);
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + sl0 * (int64_t)d * nk, ksl * nsl);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + sl0 * (int64_t)vd * nk, vsl * nsl);
+  // first key tile of each query block (the same for every slice): computed once per workgroup
+  // into LDS, so the stream's item switch is a table read, not two binary searches
+  const lds_char_t* tab = smem + kOffTab;
+  for (int qb = threadIdx.x; qb < nqb; qb += kNW * 64) {
+    int kb, ke;
+    k_range_for_q_block(a.rule, qb * kBM, min(qb * kBM + kBM, nq) - 1, &kb, &ke);
+    *reinterpret_cast<__attribute__((address_space(3))) int*>(smem + kOffTab + 4 * qb) = (kb / kBN) * kBN;
+  }
+  __syncthreads();
+  auto make_item = [&](int local) -> Item {
+    Item x;
+    const bool live = local < n_local;
+    const int64_t n = it_begin + (live ? local : 0);
+    // (64-bit division lowers to VALU code: readfirstlane keeps the results in SGPRs, else every
+    // buffer op that takes them in soffset becomes a waterfall loop)
+    x.sl = __builtin_amdgcn_readfirstlane((int)(n / nqb - sl0));
+    const int qb = __builtin_amdgcn_readfirstlane((int)(n % nqb));
+    x.q0 = live ? qb * kBM : nq;
+    const int kt0 = *reinterpret_cast<const __attribute__((address_space(3))) int*>(tab + 4 * qb);
+    x.kt0 = live ? __builtin_amdgcn_readfirstlane(kt0) : nk;
+    return x;
+  };
+  Item cur = make_item(0), nxt = make_item(1);
+  int prv_sl = 0, prv_q0 = nq;  // the finished item (none before the first)
+
+  // ---- staging lanes: this thread owns chunk `tid` of every K/V tile = 8 keys of channel row crow
+  const int cm = tid & 7, crow = tid >> 3;
+  const uint32_t goff = (uint32_t)crow * (uint32_t)nk * 2u + 16u * cm;
+  const uint32_t koff = crow < d ? goff : 0x80000000u, voff = crow < vd ? goff : 0x80000000u;
+  const uint32_t kwo = crow * 128 + ((cm * 16) ^ ((crow & 2) << 5));
+  const uint32_t vwo = crow * 128 + 16 * (cm ^ ((crow >> 1) & 7));
+  auto load = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t slb, int k0) -> u32x4 __attribute__((always_inline)) {
+    const bool in = k0 + 8 * cm < nk;
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off : 0x80000000u, slb + 2 * min(k0, nk), 0);
+  };
+  auto store = [&](int off, u32x4 v) __attribute__((always_inline)) { *reinterpret_cast<lds_u32x4_t*>(smem + off) = v; };
+  //      Q image [64][256] (64-B blocks XOR-swizzled by c&3): chunk j of a thread = channel row
+  //      (tid>>5) + 16j, 8 queries at 8*(tid&31)
+  const int qc0 = tid >> 5, qm = tid & 31;
+  const uint32_t qg_lane = (uint32_t)qc0 * (uint32_t)nq * 2u + 16u * qm;
+  const uint32_t ql_lane = qc0 * kQRow + ((qm * 16) ^ ((qc0 & 3) << 6));
+  // (inside the item loop the lane offsets are made opaque where used: hoisted per chunk they
+  // would stay live across the whole stream)
+  auto qload = [&](const Item& x, int j) -> u32x4 __attribute__((always_inline)) {
+    uint32_t qg = qg_lane;
+    int qc = qc0, qq = 8 * qm;
+    asm volatile("" : "+v"(qg), "+v"(qc), "+v"(qq));
+    const bool in = qc + 16 * j < d && x.q0 + qq < nq;
+    return __builtin_amdgcn_raw_buffer_load_b128(qrs, in ? qg + (uint32_t)j * 32u * (uint32_t)nq : 0x80000000u,
+                                                 x.sl * qsl + 2 * min(x.q0, nq), 0);
+  };
+
+  // ---- prologue: Q(item 0) into Q buffer 0, K(0..2) into ring slots 0..2, V(0..1) into slots
+  //      0..1 (slot 3 zeroed: the first PV reads "V(-1)" against P = 0), K(3..4) / V(2..3) into
+  //      the staging registers (positions 0..5 all belong to item 0: T >= 6)
+  u32x4 kst[2], vst[2];
+  {
+    u32x4 kp[3], vp[2], qv[4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) kp[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + j * kBN);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) vp[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + j * kBN);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (3 + j) * kBN);
+      vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (2 + j) * kBN);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) qv[j] = qload(cur, j);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store(ql_lane + j * 16 * kQRow, qv[j]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) store(kOffK + j * kTile + kwo, kp[j]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) store(kOffV + j * kTile + vwo, vp[j]);
+    store(kOffV + 3 * kTile + 16 * tid, u32x4{0, 0, 0, 0});
+  }
+  __syncthreads();
+
+  // Q*scale*log2(e) as the B operand of Sᵀ = Kᵀ·Q: lane (r,h) holds Q[c = 16s + 8h + e][q = 32w + r]
+  half8 qf[4];
+  auto read_q = [&](int buf) __attribute__((always_inline)) {
+    const lds_char_t* qb = smem + buf * kQImg;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int cr = 16 * s + 8 * (gq >> 1) + 4 * e + tq;
+        const int col = 32 * w + 16 * (gq & 1) + 4 * tp;
+        const half4 t = tr_read(qb + cr * kQRow + ((col * 2) ^ ((cr & 3) << 6)));
+        if (e == 0) qf[s].lo = t; else qf[s].hi = t;
+      }
+      qf[s] = scale8(qf[s], c2);
+    }
+  };
+  read_q(0);
+
+  // ---- per-item lane state (the current item's rule bounds)
+  int wq0 = 0, qi = 0, klo = 0, kspan = 0, wlo_min = 0, wlo_max = 0, whi_min = 0, whi_max = 0;
+  bool wave_active = false;
+  auto item_state = [&](const Item& x) __attribute__((always_inline)) {
+    wq0 = x.q0 + 32 * w;
+    qi = wq0 + r;
+    wave_active = wq0 < nq;
+    klo = 0; kspan = 0; wlo_min = wlo_max = whi_min = whi_max = 0;
+    if (wave_active) {
+      int khi;
+      const Rule& R = a.rule;
+      if (R.k.s0 == 1) {  // unit key stride (none_front, or Nk >= Nq): the interval in closed form
+        const int qo = R.q.o0 + R.q.s0 * min(qi, nq - 1);
+        const int ohi = R.look_ahead == 1 ? qo : sat_add32(qo, R.ws - 1);
+        klo = min(max(qo - (R.ws - 1) - R.k.o0, 0), nk);
+        khi = min(ohi - R.k.o0, nk - 1);
+      } else {
+        key_interval(R, min(qi, nq - 1), &klo, &khi);
+      }
+      kspan = max(khi - klo + 1, 0);
+      const int last = min(31, nq - 1 - wq0);
+      wlo_min = __builtin_amdgcn_readfirstlane(klo);
+      whi_min = __builtin_amdgcn_readfirstlane(khi);
+      wlo_max = __builtin_amdgcn_readlane(klo, last);
+      whi_max = __builtin_amdgcn_readlane(khi, last);
+    }
+  };
+  item_state(cur);
+  // tile class of position `it` of the current item: 0 no allowed pair, 1 mixed, 2 all allowed
+  auto tcls = [&](int it) -> int __attribute__((always_inline)) {
+    const int k0 = cur.kt0 + it * kBN, k1 = k0 + kBN - 1;
+    if (!wave_active || wlo_min > k1 || whi_max < k0) return 0;
+    return (wlo_max <= k0 && whi_min >= k1 && k1 < nk) ? 2 : 1;
+  };
+
+  // fragment read bases (lane constants), as fa_fwd_f16_pingpong.hip
+  const int sig = ((tp & 1) << 1) | (tp >> 1);
+  uint32_t kbase[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    kbase[t] = (8 * (gq >> 1) + tq) * 128 + (((32 * t + 16 * (gq & 1) + 4 * sig) * 2) ^ ((tq & 2) << 5));
+  uint32_t vbase[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) vbase[s] = r * 128 + 16 * ((2 * s + h) ^ ((r >> 1) & 7));
+
+  auto read_kstep = [&](const lds_char_t* p, int s, half8 (&f)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f[t].lo = tr_read(p + kbase[t] + (16 * s) * 128);
+      f[t].hi = tr_read(p + kbase[t] + (16 * s + 4) * 128);
+    }
+  };
+  auto read_vstep = [&](const lds_char_t* p, int s, half8 (&f)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) f[u] = read_b128(p + vbase[s] + 32 * u * 128);
+  };
+
+  floatx16 st[2];      // Sᵀ of the tile being softmaxed
+  uint32_t pw[4][4];   // P (fp16 pairs), dword x of PV k-step s
+  floatx16 o[2];       // Oᵀ: channels 32u + 8(i>>2) + 4h + (i&3)
+  floatx16 negm;       // -m_run broadcast: the C operand of every Sᵀ chain
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) pw[x][y] = 0u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.f;
+    o[1][i] = 0.f;
+    negm[i] = 0.f;
+  }
+  float m_run = 0.f, m_max = kNegInf, thr = -__FLT_MAX__;
+  float lacc[4] = {0.f, 0.f, 0.f, 0.f};
+
+  auto mask = [&](int k0) __attribute__((always_inline)) {
+    const int base = k0 + 8 * h - klo;  // allowed iff base + o in [0, kspan)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int off = 32 * t + 16 * (i >> 3) + (i & 7);
+        st[t][i] = ((unsigned)(base + off) < (unsigned)kspan) ? st[t][i] : kNegInf;
+      }
+  };
+  auto exp_cvt = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const float s0 = st[s >> 1][8 * (s & 1) + 2 * x], s1 = st[s >> 1][8 * (s & 1) + 2 * x + 1];
+        pw[s][x] = __builtin_bit_cast(uint32_t, half2v{(_Float16)__builtin_amdgcn_exp2f(s0),
+                                                       (_Float16)__builtin_amdgcn_exp2f(s1)});
+      }
+  };
+  auto softmax = [&](int it, int cls, bool first) __attribute__((always_inline)) {
+    if (cls == 1) mask(cur.kt0 + it * kBN);
+    float mx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mx[j] = fmaxf(st[j >> 1][8 * (j & 1)], st[j >> 1][8 * (j & 1) + 1]);
+#pragma unroll
+    for (int i = 2; i < 8; i += 2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        mx[j] = fmaxf(fmaxf(mx[j], st[j >> 1][8 * (j & 1) + i]), st[j >> 1][8 * (j & 1) + i + 1]);
+    const float mt = max_pair32(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
+    m_max = fmaxf(m_max, m_run + mt);
+    if (first) {  // an item's first tile: nothing to rescale (O and l start fresh): seed, then exp once
+      const bool seed = mt > -__FLT_MAX__;  // else (an empty row so far) a later tile seeds
+      const float delta = seed ? mt : 0.f;
+      m_run += delta;
+      thr = seed ? kRescaleThr : -__FLT_MAX__;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        st[0][i] -= delta;
+        st[1][i] -= delta;
+        negm[i] = -m_run;
+      }
+      exp_cvt();
+    } else {
+    exp_cvt();
+#pragma unroll
+    for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
+      asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
+    if (__any(mt > thr)) {
+      const bool unset = thr < 0.f;
+      const bool seed = unset && (mt > thr);
+      const float delta = unset ? (seed ? mt : 0.f) : fmaxf(mt, 0.f);
+      const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
+      m_run += delta;
+      thr = (unset && !seed) ? thr : kRescaleThr;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) lacc[x] *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o[0][i] *= alpha;
+        o[1][i] *= alpha;
+        st[0][i] -= delta;
+        st[1][i] -= delta;
+        negm[i] = -m_run;
+      }
+      exp_cvt();
+    }
+    }
+    const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int x = 0; x < 4; ++x)  // an item's first tile starts the sums (no reset at the boundary)
+        lacc[x] = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2v, pw[s][x]), one2, (first && s == 0) ? 0.f : lacc[x],
+                                         false);
+  };
+
+  int n = 0;  // local item index (positions of the item are static in the unrolled body)
+
+  // O, l, m of the item that just finished (its last PV ran in the MFMA phase before) into LDS:
+  // O [c][256 q] fp16 over the finished item's Q buffer, l / m at the l/m area
+  auto epilogue_lds = [&]() __attribute__((always_inline)) {
+    const float l_tot = sum_pair32((lacc[0] + lacc[1]) + (lacc[2] + lacc[3]));
+    const float inv = (l_tot > 0.f) ? __builtin_amdgcn_rcpf(l_tot) : 0.f;
+    lds_char_t* ob = smem + ((n + 1) & 1) * kQImg + 2 * (32 * w + r);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int cch = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+        *reinterpret_cast<__attribute__((address_space(3))) _Float16*>(ob + cch * kQRow) = (_Float16)(o[u][i] * inv);
+        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // a few values at a time (register peak)
+      }
+    if (h == 0) {
+      float lv = 0.f;
+      __half mv = neg_inf_approx<__half>();
+      if (l_tot > 0.f) {
+        mv = __float2half(m_max * kLn2);
+        // l relative to the STORED (rounded) m, so exp(s - m)/l is exact downstream
+        lv = l_tot * __builtin_amdgcn_exp2f(m_run - __half2float(mv) * kLog2e);
+      }
+      *reinterpret_cast<__attribute__((address_space(3))) float*>(smem + kOffLM + 4 * (32 * w + r)) = lv;
+      *reinterpret_cast<__attribute__((address_space(3))) unsigned short*>(smem + kOffLM + 4 * kBM + 2 * (32 * w + r)) =
+          __half_as_ushort(mv);
+    }
+  };
+
+  // Q chunks of the next item (one per phase, loaded at positions 2-5, stored two positions later)
+  u32x4 qst[2];
+  // the finished item's O / l / m leave from LDS at positions 2-3: lane constants
+  const int orow = tid >> 5, ocol = tid & 31;  // 16-B chunk (c = orow + 16j, queries 8*ocol..)
+  const uint32_t osl = 2u * vd * nq;  // bytes per O slice
+  const __amdgpu_buffer_rsrc_t ors = make_rsrc(static_cast<__half*>(a.O) + sl0 * (int64_t)vd * nq, osl * nsl);
+  const __amdgpu_buffer_rsrc_t lrs = make_rsrc(static_cast<float*>(a.l) + sl0 * (int64_t)nq, 4u * nq * nsl);
+  const __amdgpu_buffer_rsrc_t mrs = make_rsrc(static_cast<__half*>(a.m) + sl0 * (int64_t)nq, 2u * nq * nsl);
+
+  // MFMA(it) (ring slot c = it mod 4): Sᵀ of the tile with K (k-steps 0-1 prefetched, 2-3 read
+  // here), PV of the previous tile with its V (read here, two k-steps ahead of their MFMAs), the
+  // next tile's K k-steps 0-1; staging: K(+3) / V(+2) into the ring over K(-1) / V(-2), loads of
+  // K(+5) / V(+4); the item's fixed-position traffic (O / l / m out at 2-3, the next item's Q in
+  // at 2-3 and into LDS at 4-5)
+  auto mfma_phase = [&](auto IT_) __attribute__((always_inline)) {
+    constexpr int it = decltype(IT_)::value;
+    constexpr int c = it & 3, x = it & 1;
+    __builtin_amdgcn_s_setprio(1);
+    const lds_char_t* pk = smem + kOffK + c * kTile;
+    const lds_char_t* pkn = smem + kOffK + ((c + 1) & 3) * kTile;
+    const lds_char_t* pv = smem + kOffV + ((c + 3) & 3) * kTile;
+    // every fragment is read in the phase that uses it, two k-steps ahead (nothing lives across
+    // the VALU phase: the register budget holds the stream's staging); the first two K k-steps
+    // are read at the phase start, their latency the only one exposed
+    half8 kf[4][2], vf[4][2];
+    read_kstep(pk, 0, kf[0]);
+    read_kstep(pk, 1, kf[1]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[s][t], qf[s], s == 0 ? negm : st[t], 0, 0, 0);
+      if (s < 2) read_kstep(pk, s + 2, kf[s + 2]);
+      else read_vstep(pv, s - 2, vf[s - 2]);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const half8 pp = __builtin_bit_cast(half8, u32x4{pw[s][0], pw[s][1], pw[s][2], pw[s][3]});
+      // position 1 holds an item's first PV (tile 0): it starts the accumulator (the finished
+      // item's O left for LDS in the VALU phase before; no reset keeps both alive)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], pp, (it == 1 && s == 0) ? floatx16{} : o[u], 0, 0, 0);
+      if (s < 2) read_vstep(pv, s + 2, vf[s + 2]);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // K k-steps 0-1
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // Sᵀ k-steps 0-1, each followed by a K k-step's reads
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {  // Sᵀ k-steps 2-3 and PV k-steps 0-1, each followed by a V k-step
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // PV k-steps 2-3
+    // staging: K(+3), V(+2) into the ring; loads of K(+5), V(+4) (this item's or the next's)
+    store(kOffK + ((c + 3) & 3) * kTile + kwo, kst[x]);
+    store(kOffV + ((c + 2) & 3) * kTile + vwo, vst[x]);
+    if constexpr (it >= 4 && it <= 7) {  // the next item's Q chunk j = it-4 over the finished item's O
+      uint32_t ql = ql_lane;
+      asm volatile("" : "+v"(ql));
+      store(((n + 1) & 1) * kQImg + ql + (it - 4) * 16 * kQRow, qst[x]);
+    }
+    if constexpr (it == 2 || it == 3) {  // the finished item's O rows (at 2 also l / m); none before item 1
+      const bool on = prv_q0 < nq;
+      const lds_char_t* ob = smem + ((n + 1) & 1) * kQImg;
+      int orw = orow, ocl = ocol, tt = tid;
+      asm volatile("" : "+v"(orw), "+v"(ocl), "+v"(tt));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cc = orw + 16 * (2 * (it & 1) + j);
+        const u32x4 v = *reinterpret_cast<const lds_u32x4_t*>(ob + cc * kQRow + 16 * ocl);
+        const bool in = on && prv_q0 + 8 * ocl < nq;
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, in ? (uint32_t)cc * (uint32_t)nq * 2u + 16u * ocl : 0x80000000u,
+                                               prv_sl * osl + 2 * min(prv_q0, nq), 0);
+      }
+      if constexpr (it == 2) {
+        const u32x4 v = *reinterpret_cast<const lds_u32x4_t*>(smem + kOffLM + 16 * (tt % 96));
+        const uint32_t loff = (on && tt < 64 && prv_q0 + 4 * tt < nq) ? 16u * tt : 0x80000000u;
+        const uint32_t moff = (on && tt >= 64 && tt < 96 && prv_q0 + 8 * (tt - 64) < nq) ? 16u * (tt - 64) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(v, lrs, loff, prv_sl * 4 * nq + 4 * min(prv_q0, nq), 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, mrs, moff, prv_sl * 2 * nq + 2 * min(prv_q0, nq), 0);
+      }
+    }
+    if constexpr (it >= 2 && it <= 5) qst[x] = qload(nxt, it - 2);
+    if constexpr (it + 5 < T) kst[x] = load(krs, koff, cur.sl * ksl, cur.kt0 + (it + 5) * kBN);
+    else kst[x] = load(krs, koff, nxt.sl * ksl, nxt.kt0 + (it + 5 - T) * kBN);
+    if constexpr (it + 4 < T) vst[x] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (it + 4) * kBN);
+    else vst[x] = load(vrs, voff, nxt.sl * vsl, nxt.kt0 + (it + 4 - T) * kBN);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // VALU(it): [position 0 past the first item: O / l / m of the finished item into LDS, the new
+  // item's lane state] softmax of the tile; [last position: the next item's Q fragments]
+  auto valu_phase = [&](auto IT_) __attribute__((always_inline)) {
+    constexpr int it = decltype(IT_)::value;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's staging stores / reads landed
+    if constexpr (it == 0) {
+      if (n > 0) {
+        epilogue_lds();
+        __builtin_amdgcn_sched_barrier(0);  // the epilogue's temporaries die before the softmax's
+        m_max = kNegInf;
+        thr = -__FLT_MAX__;  // the item's first allowed key seeds m_run (scores are relative to it)
+        item_state(cur);
+      }
+    }
+    const int cls = tcls(it);
+    if (cls != 0) {
+      softmax(it, cls, it == 0);
+    } else {  // the next (unconditional) PV must add nothing
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int z = 0; z < 4; ++z) pw[y][z] = 0u;
+      if constexpr (it == 0) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) lacc[y] = 0.f;
+      }
+    }
+    if constexpr (it == T - 1) read_q((n + 1) & 1);  // before this wave's first Sᵀ of the next item
+  };
+
+  const int grp = w >> 2;  // waves w and w+4 share a SIMD
+  if (grp == 1) __builtin_amdgcn_s_barrier();
+  // diagnostic build only (STAMP): s_memtime of waves 0 and 4 of workgroup 0 at the four phase
+  // edges of every position of its first four items, written over the last slice's Q (WRONG)
+  auto stamp = [&](int it, int k) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      if (blockIdx.x == 0 && (w == 0 || w == 4) && lane == 0 && n < 4) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        // (into the LAST slice's Q: no store of this workgroup lands there)
+        uint64_t* dbg = reinterpret_cast<uint64_t*>(const_cast<void*>(a.Q)) + (a.b - 1) * (int64_t)d * nq / 4;
+        dbg[((n * T + it) * 4 + k) * 2 + (w >> 2)] = t;
+      }
+    }
+  };
+  auto step = [&](auto IT_) __attribute__((always_inline)) {
+    constexpr int it = decltype(IT_)::value;
+    if constexpr (it == 0) {
+      if (n > 0) {  // shift the item window (wave-uniform scalars)
+        prv_sl = cur.sl;
+        prv_q0 = cur.q0;
+        cur = nxt;
+        nxt = make_item(n + 1);
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+    stamp(it, 0);
+    mfma_phase(IT_);
+    stamp(it, 1);
+    __builtin_amdgcn_s_barrier();
+    stamp(it, 2);
+    valu_phase(IT_);
+    stamp(it, 3);
+  };
+  // one extra (phantom) item at the end: its positions 0-3 carry the last item's PV, its O / l /
+  // m into LDS and out to HBM; the rest only move zeros
+  for (n = 0; n <= n_local; ++n) static_for<0, T>(step);
+  if (grp == 0) __builtin_amdgcn_s_barrier();
+}
+
+int g_cus = 0;
+
+int64_t band_workgroups(int64_t n_items) {
+  if (g_cus == 0) {
+    int dev = 0, cus = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    g_cus = cus;
+  }
+  return n_items < g_cus ? n_items : g_cus;
+}
+
+struct TCache {
+  Rule r;
+  int T;
+  bool valid;
+};
+thread_local TCache g_tcache = {{}, 0, false};
+
+}  // namespace
+
+int band_tiles_per_item(const FwdArgs& a) {
+  if (g_tcache.valid && !memcmp(&g_tcache.r, &a.rule, sizeof(Rule))) return g_tcache.T;
+  const int nq = a.rule.q.n;
+  const int nqb = (nq + kBM - 1) / kBM;
+  int T = 0;
+  for (int qb = 0; qb < nqb; ++qb) {  // host: exact per block (two binary searches each)
+    int kb, ke;
+    const int q0 = qb * kBM;
+    k_range_for_q_block(a.rule, q0, min(q0 + kBM, nq) - 1, &kb, &ke);
+    if (ke > kb) T = max(T, (ke - (kb / kBN) * kBN + kBN - 1) / kBN);
+  }
+  T = (max(T, kMinT) + 3) / 4 * 4;  // a multiple of 4: ring slots are static per position
+  g_tcache.r = a.rule;
+  g_tcache.T = T;
+  g_tcache.valid = true;
+  return T;
+}
+
+bool fwd_f16_band_supported(const FwdArgs& a) {
+  const Rule& r = a.rule;
+  const int nq = r.q.n, nk = r.k.n;
+  const int dm = max(a.d, a.v_d);
+  if (!(r.policy == 2 && r.seq_dims == 1 && r.ls == 0)) return false;
+  // v_d == 64: the epilogue's per-value buffer stores need no channel predicate (a predicated
+  // form keeps 32 lane-dependent 64-bit offsets live across the stream: 116 spilled VGPRs)
+  if (!(a.v_d == kD && a.d > 32 && a.d <= kD && nk % 8 == 0 && nk > 0 && nq > 0)) return false;
+  if ((int64_t)dm * nk * 2 >= (1ll << 31) || (int64_t)dm * nq * 2 >= (1ll << 31)) return false;
+  if ((reinterpret_cast<uintptr_t>(a.K) % 16) || (reinterpret_cast<uintptr_t>(a.V) % 16) ||
+      (reinterpret_cast<uintptr_t>(a.Q) % 16) || nq % 8)
+    return false;
+  // a band: every block spans few tiles (else the per-launch kernels cover it at no loss)
+  if (band_tiles_per_item(a) > 24) return false;
+  // one descriptor per tensor spans a workgroup's slices: below 2^31 bytes
+  const int64_t nqb = (nq + kBM - 1) / kBM, n_items = a.b * nqb, n_wg = band_workgroups(n_items);
+  const int64_t span = (n_items + n_wg - 1) / n_wg / nqb + 2;
+  return span * 2 * (int64_t)dm * (nq > nk ? nq : nk) < (1ll << 31);
+}
+
+template <int T, bool STAMP = false>
+hipError_t launch_band_t(const BandArgs& ba, hipStream_t s) {
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(fwd_f16_band_kernel<T, STAMP>), kSmem);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((fwd_f16_band_kernel<T, STAMP>), dim3((unsigned)ba.n_wg), dim3(kNW * 64), kSmem, s, ba);
+  return hipGetLastError();
+}
+
+hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
+  BandArgs ba;
+  ba.a = a;
+  ba.T = band_tiles_per_item(a);
+  ba.n_items = a.b * (int64_t)((a.rule.q.n + kBM - 1) / kBM);
+  ba.n_wg = (int)band_workgroups(ba.n_items);
+#ifdef FA_DIAG
+  if (diag_variant("FA_FWD_VARIANT") == 2401 && ba.T == 12) return launch_band_t<12, true>(ba, s);
+#endif
+  switch (ba.T) {
+    case 12: return launch_band_t<12>(ba, s);
+    case 16: return launch_band_t<16>(ba, s);
+    case 20: return launch_band_t<20>(ba, s);
+    default: return launch_band_t<24>(ba, s);
+  }
+}
+
+}  // namespace fa

@@ -550,9 +550,12 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
     }
   }
   const bool tuned = v < 0;
+  if ((v == 2400 || v == 2401) && fwd_f16_band_supported(a)) return launch_fwd_f16_band(a, s);
 #else
   constexpr bool tuned = true;
 #endif
+  // 1d local windows at d <= 64: the persistent band kernel (no per-block start / end cost)
+  if (tuned && fwd_f16_band_supported(a)) return launch_fwd_f16_band(a, s);
   // ping-pong kernel (two wave groups alternating MFMA / softmax phases): the default for
   // d <= 64 under the full policy (c2: 948 vs 904 TF/s for the 8-wave kernel below)
   if (tuned && a.rule.policy == 0 && fwd_f16_pingpong_supported(a)) return launch_fwd_f16_pingpong(a, s);

@@ -78,6 +78,16 @@ constexpr int kFIlvFine = 16384;  // ... one MFMA at a time (2 / 1 reads after e
 constexpr int kFIlvStores = 32768;  // ... and the staging stores / loads pinned after the 2nd MFMA pair of each half
 constexpr int kFIlvAt0 = 65536;     // ... (after the 1st pair)
 constexpr int kFIlvAt2 = 131072;    // ... (after the 3rd pair)
+// row sums into four running fp32 accumulators that live across tiles (rescaled at a rebase),
+// instead of four per-tile chains folded into l0 / l1: 10 fewer VALU per tile
+constexpr int kFSumsAcc = 262144;
+// (with kFSumsAcc) the tile's row sums as fp32 adds of the exponentials inside exp_cvt instead of
+// v_dot2c on the packed P (v_dot2c is priced well above a plain add beside MFMAs)
+constexpr int kFSumsF32 = 524288;
+// the per-tile rebase check on this lane's half of the row (32 keys) with no cross-lane step; the
+// exact row max is formed only inside the (rare) rebase branch, and the m output's running max
+// stays per lane until the epilogue combines the two halves once
+constexpr int kFHalfMax = 1048576;
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
@@ -315,8 +325,23 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         st[t][i] = ok ? st[t][i] : kNegInf;
       }
   };
+  float lacc[4] = {0.f, 0.f, 0.f, 0.f};  // kFSumsAcc: running row sums (chains x = 0..3)
+  float ts[4];                            // kFSumsF32: this tile's row sums (four chains)
   auto row_sums = [&]() __attribute__((always_inline)) {
     const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
+    if constexpr ((F & kFSumsF32) != 0) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) lacc[x] += ts[x];
+      return;
+    }
+    if constexpr ((F & kFSumsAcc) != 0) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+          lacc[x] = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2v, pw[s][x]), one2, lacc[x], false);
+      return;
+    }
     float ls[4] = {0.f, 0.f, 0.f, 0.f};  // four chains, folded into l0 / l1 once
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -331,6 +356,12 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         const float s0 = st[s >> 1][8 * (s & 1) + 2 * x], s1 = st[s >> 1][8 * (s & 1) + 2 * x + 1];
+        if constexpr ((F & kFSumsF32) != 0) {
+          const float e0 = __builtin_amdgcn_exp2f(s0), e1 = __builtin_amdgcn_exp2f(s1);
+          pw[s][x] = __builtin_bit_cast(uint32_t, half2v{(_Float16)e0, (_Float16)e1});
+          ts[x] = (s == 0) ? e0 + e1 : ts[x] + e0 + e1;
+          continue;
+        }
         pw[s][x] = (F & kANoExp) ? __builtin_bit_cast(uint32_t, half2v{(_Float16)s0, (_Float16)s1})
                                  : __builtin_bit_cast(uint32_t, half2v{(_Float16)__builtin_amdgcn_exp2f(s0),
                                                                        (_Float16)__builtin_amdgcn_exp2f(s1)});
@@ -349,21 +380,28 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         mx[j] = fmaxf(fmaxf(mx[j], st[j >> 1][8 * (j & 1) + i]), st[j >> 1][8 * (j & 1) + i + 1]);
-    const float mt = (F & kANoMax) ? -1.f : max_pair32(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
+    constexpr bool HALF = (F & kFHalfMax) != 0;
+    const float mth = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
+    const float mt = (F & kANoMax) ? -1.f : (HALF ? mth : max_pair32(mth));
     m_max = fmaxf(m_max, m_run + mt);
     exp_cvt();
 #pragma unroll
     for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
       asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
     if (__any(mt > thr)) {
+      const float mtf = HALF ? max_pair32(mth) : mt;  // the whole row's tile max
       const bool unset = thr < 0.f;
-      const bool seed = unset && (mt > thr);
-      const float delta = unset ? (seed ? mt : 0.f) : fmaxf(mt, 0.f);
+      const bool seed = unset && (mtf > thr);
+      const float delta = unset ? (seed ? mtf : 0.f) : fmaxf(mtf, 0.f);
       const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
       m_run += delta;
       thr = (unset && !seed) ? thr : kRescaleThr;
       l0 *= alpha;
       l1 *= alpha;
+      if constexpr ((F & kFSumsAcc) != 0) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) lacc[x] *= alpha;
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         o[0][i] *= alpha;
@@ -563,6 +601,8 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
 
   // ---- epilogue
   if (!wave_active) return;
+  if constexpr ((F & kFSumsAcc) != 0) l0 = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
+  if constexpr ((F & kFHalfMax) != 0) m_max = max_pair32(m_max);
   const float l_tot = sum_pair32(l0 + l1);
   const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
   if (qi >= nq) return;
@@ -650,8 +690,11 @@ bool fwd_f16_pingpong_supported(const FwdArgs& a) {
 }
 
 // tuned (c2, MI355X): MFMA phases at priority 1, fragment reads and staging interleaved with
-// the MFMAs (full policy; 0.5526-0.5716 ms against 0.595 for 2206)
-constexpr int kFDefault = kFPrio | kFStoresLate | kFInterleave | kFIlvStores;
+// the MFMAs (full policy; 0.5526-0.5716 ms against 0.595 for 2206), row sums in running
+// accumulators (0.5451 against 0.5552 ms in one process; fp32 adds instead of v_dot2c: 0.5812
+// against 0.5690; the half-row rebase check kFHalfMax: 0.5464, no gain)
+constexpr int kFDefaultR1 = kFPrio | kFStoresLate | kFInterleave | kFIlvStores;
+constexpr int kFDefault = kFDefaultR1 | kFSumsAcc;
 
 hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
 #ifdef FA_DIAG
@@ -688,6 +731,9 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2267: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag>(a, s);
     case 2268: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
     case 2201: return launch_t<kFPrio>(a, s);
+    case 2290: return launch_t<kFDefaultR1>(a, s);  // round-1 default (per-tile row-sum chains)
+    case 2291: return launch_t<kFDefault | kFSumsF32>(a, s);
+    case 2292: return launch_t<kFDefault | kFHalfMax>(a, s);
     default: break;
   }
 #endif

@@ -64,6 +64,10 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s);
 // ping-pong fp16 forward for 64 < max(d, v_d) <= 128 — fa_fwd_f16_pingpong128.hip
 bool fwd_f16_pingpong128_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_pingpong128(const FwdArgs& a, hipStream_t s);
+// persistent band forward for 1d unit-stride local windows, 32 < max(d, v_d) <= 64 — fa_fwd_f16_band.hip
+bool fwd_f16_band_supported(const FwdArgs& a);
+int band_tiles_per_item(const FwdArgs& a);
+hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s);
 bool bwd_f16_supported(const BwdArgs& a);
 // fp32 MFMA forward — fa_fwd_f32.hip
 bool fwd_f32_supported(const FwdArgs& a);
