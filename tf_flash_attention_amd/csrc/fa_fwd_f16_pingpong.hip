@@ -27,7 +27,9 @@
 // XOR-swizzled by (c>>1)&7).  Rings of three slots for K and V.
 //
 // Numerics as fa_fwd_f16.hip (fp32 accumulation, log2-domain lazy rebase at 8, l
-// relative to the stored fp16 m).  Replaces the reference's ForwardImpl
+// relative to the stored fp16 m), except that the rebase check runs on the packed fp16
+// exponentials (kFPMax): m is exact for tiles that rebased and m_run + log2(max P) for the
+// others (< 4.9e-4 from the exact max).  Replaces the reference's ForwardImpl
 // (flash_attention.cu:425-1077) for these shapes.
 #include "fa_device.h"
 #include "fa_kernels.h"
@@ -88,6 +90,12 @@ constexpr int kFSumsF32 = 524288;
 // exact row max is formed only inside the (rare) rebase branch, and the m output's running max
 // stays per lane until the epilogue combines the two halves once
 constexpr int kFHalfMax = 1048576;
+// rebase check and m on P: the tile max is taken over the packed fp16 exponentials (8
+// v_pk_maximum3_f16 instead of 16 fp32 max3 plus a cross-lane step), tested against 2^thr; the
+// exact fp32 row max is formed only in the (rare) rebase branch.  m = m_run + log2(max P) for the
+// tiles of the current epoch (fp16 rounding of P: |error| <= 2^-11 log2(e) in log2 units, i.e.
+// < 4.9e-4 in m), exact for the tiles that rebased.
+constexpr int kFPMax = 1 << 22;
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
@@ -312,6 +320,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
     negm[i] = 0.f;
   }
   float m_run = 0.f, l0 = 0.f, l1 = 0.f, m_max = kNegInf, thr = -__FLT_MAX__;
+  constexpr bool PMAX = (F & kFPMax) != 0;
+  half2v pmr = {(_Float16)0.f, (_Float16)0.f};  // PMAX: running max of P over the current epoch (per lane)
+  _Float16 thr_h = (_Float16)-1.f;              // PMAX: 2^thr once seeded; -1 (always exceeded) before
 
   auto mask = [&](int k0) __attribute__((always_inline)) {
     const int lim = nk - k0 - 8 * h;       // POL 0: offset o is in range iff o < lim
@@ -369,7 +380,73 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   };
   // softmax of tile `it`: the exponentials are computed speculatively against m_run beside the
   // row max; only a seed or a max past the threshold (rare) rebases O, l, Sᵀ, -m and redoes them
+  auto pmax_tile = [&]() -> half2v __attribute__((always_inline)) {
+    auto M3 = [](half2v x, half2v y, half2v z) __attribute__((always_inline)) {
+      return __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z);
+    };
+    auto H = [&](int s_, int x) __attribute__((always_inline)) { return __builtin_bit_cast(half2v, pw[s_][x]); };
+    half2v a0 = M3(H(0, 0), H(0, 1), H(0, 2)), b0 = M3(H(2, 0), H(2, 1), H(2, 2));
+    a0 = M3(a0, H(0, 3), H(1, 0));
+    b0 = M3(b0, H(2, 3), H(3, 0));
+    a0 = M3(a0, H(1, 1), H(1, 2));
+    b0 = M3(b0, H(3, 1), H(3, 2));
+    return M3(M3(a0, H(1, 3), H(3, 3)), b0, b0);
+  };
+  auto softmax_p = [&](int it, int cls) __attribute__((always_inline)) {
+    if (cls == 1) mask(kt0 + it * kBN);
+    exp_cvt();
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
+    const half2v tm = pmax_tile();
+    const _Float16 tmx = __builtin_elementwise_maximum(tm[0], tm[1]);
+    const half2v pmr_old = pmr;
+    pmr = __builtin_elementwise_maximum(pmr, tm);
+    if (__any(tmx > thr_h)) {
+      // the exact fp32 row max of this tile (relative to m_run), both key halves
+      float mx[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mx[j] = fmaxf(st[j >> 1][8 * (j & 1)], st[j >> 1][8 * (j & 1) + 1]);
+#pragma unroll
+      for (int i = 2; i < 8; i += 2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          mx[j] = fmaxf(fmaxf(mx[j], st[j >> 1][8 * (j & 1) + i]), st[j >> 1][8 * (j & 1) + i + 1]);
+      const float mtf = max_pair32(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
+      // close the epoch: its P maximum (approximate) and this tile (exact) into m_max
+      const float pold = (float)__builtin_elementwise_maximum(pmr_old[0], pmr_old[1]);
+      m_max = fmaxf(m_max, fmaxf(m_run + mtf, m_run + __log2f(pold)));
+      const bool unset = thr < 0.f;
+      const bool seed = unset && (mtf > thr);
+      const float delta = unset ? (seed ? mtf : 0.f) : fmaxf(mtf, 0.f);
+      const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
+      m_run += delta;
+      thr = (unset && !seed) ? thr : kRescaleThr;
+      thr_h = (unset && !seed) ? (_Float16)-1.f : (_Float16)(1 << (int)kRescaleThr);
+      if constexpr ((F & kFSumsAcc) != 0) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) lacc[x] *= alpha;
+      }
+      l0 *= alpha;
+      l1 *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o[0][i] *= alpha;
+        o[1][i] *= alpha;
+        st[0][i] -= delta;
+        st[1][i] -= delta;
+        negm[i] = -m_run;
+      }
+      exp_cvt();
+      pmr = half2v{(_Float16)0.f, (_Float16)0.f};
+    }
+    if (!(F & (kFSumsLate | kANoSums))) row_sums();
+  };
   auto softmax = [&](int it, int cls) __attribute__((always_inline)) {
+    if constexpr (PMAX) {
+      softmax_p(it, cls);
+      return;
+    }
     if (cls == 1) mask(kt0 + it * kBN);
     // four independent max3 chains (one wave does the VALU work on its SIMD: latency shows)
     float mx[4];
@@ -603,6 +680,8 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   if (!wave_active) return;
   if constexpr ((F & kFSumsAcc) != 0) l0 = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
   if constexpr ((F & kFHalfMax) != 0) m_max = max_pair32(m_max);
+  if constexpr (PMAX)
+    m_max = max_pair32(fmaxf(m_max, m_run + __log2f((float)__builtin_elementwise_maximum(pmr[0], pmr[1]))));
   const float l_tot = sum_pair32(l0 + l1);
   const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
   if (qi >= nq) return;
@@ -692,9 +771,11 @@ bool fwd_f16_pingpong_supported(const FwdArgs& a) {
 // tuned (c2, MI355X): MFMA phases at priority 1, fragment reads and staging interleaved with
 // the MFMAs (full policy; 0.5526-0.5716 ms against 0.595 for 2206), row sums in running
 // accumulators (0.5451 against 0.5552 ms in one process; fp32 adds instead of v_dot2c: 0.5812
-// against 0.5690; the half-row rebase check kFHalfMax: 0.5464, no gain)
+// against 0.5690; the half-row rebase check kFHalfMax: 0.5464, no gain), rebase check and m on
+// the packed P (0.5395-0.5441 against 0.5512-0.5553 ms in one process)
 constexpr int kFDefaultR1 = kFPrio | kFStoresLate | kFInterleave | kFIlvStores;
-constexpr int kFDefault = kFDefaultR1 | kFSumsAcc;
+constexpr int kFDefaultR2 = kFDefaultR1 | kFSumsAcc;
+constexpr int kFDefault = kFDefaultR2 | kFPMax;
 
 hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
 #ifdef FA_DIAG
@@ -732,8 +813,12 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2268: return launch_t<kFPrio | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
     case 2201: return launch_t<kFPrio>(a, s);
     case 2290: return launch_t<kFDefaultR1>(a, s);  // round-1 default (per-tile row-sum chains)
-    case 2291: return launch_t<kFDefault | kFSumsF32>(a, s);
-    case 2292: return launch_t<kFDefault | kFHalfMax>(a, s);
+    case 2291: return launch_t<kFDefaultR2 | kFSumsF32>(a, s);
+    case 2292: return launch_t<kFDefaultR2 | kFHalfMax>(a, s);
+    case 2293: return launch_t<kFDefaultR2>(a, s);  // round-2 default (exact fp32 row max every tile)
+    case 2297: return launch_t<kFDefault | kANoExp>(a, s);             // timing only: no exp2 (outputs wrong)
+    case 2298: return launch_t<kFDefault | kANoLoad | kANoStore>(a, s);  // timing only: no staging
+    case 2299: return launch_t<kFDefault | kFStamp>(a, s);
     default: break;
   }
 #endif
