@@ -65,8 +65,18 @@ def _call(policy, seq_dims, tq, tk, tv, mode, ws, ls, causal):
     return f(tq, tk, tv, ws, ls, causal, mode, returning_l_m=True)
 
 
+def _to_dev(x, dev, bwd, misalign):
+    t = torch.from_numpy(x).to(dev)
+    if misalign:  # same values at a data pointer one element past an aligned allocation
+        buf = torch.empty(t.numel() + 1, dtype=t.dtype, device=dev)
+        buf[1:].copy_(t.reshape(-1))
+        t = buf[1:].view(t.shape)
+        assert t.is_contiguous() and t.data_ptr() % 16 != 0
+    return t.requires_grad_(bwd)
+
+
 def run_case(dtype, policy, seq_dims, mode, batch, d, vd, qs, ks, ws=1, ls=0, causal=False, seed=0, bwd=True,
-             slices=None, inputs=None):
+             slices=None, inputs=None, misalign=False):
     rng = np.random.default_rng(seed)
     qs, ks = tuple(qs), tuple(ks)
     if inputs is None:
@@ -77,9 +87,7 @@ def run_case(dtype, policy, seq_dims, mode, batch, d, vd, qs, ks, ws=1, ls=0, ca
     else:
         Q, K, V, dO = inputs
     dev = torch.device("cuda:0")
-    tq = torch.from_numpy(Q).to(dev).requires_grad_(bwd)
-    tk = torch.from_numpy(K).to(dev).requires_grad_(bwd)
-    tv = torch.from_numpy(V).to(dev).requires_grad_(bwd)
+    tq, tk, tv = (_to_dev(x, dev, bwd, misalign) for x in (Q, K, V))
     o, l, m = _call(policy, seq_dims, tq, tk, tv, mode, ws, ls, causal)
     if bwd:
         o.backward(torch.from_numpy(dO).to(dev))
@@ -212,6 +220,26 @@ def test_f16_mfma_shapes(d, policy, nq, nk):
 ])
 def test_f16_fast_paths(d, policy, ws, causal, seq_dims, mode, qs, ks):
     run_case(np.float16, policy, seq_dims, mode, (2, 2), d, d, qs, ks, ws=ws, ls=0, causal=causal, seed=d + ws)
+
+
+# the two-pass fp16 backward beyond the interval rules and aligned lengths: strided and 2d local
+# windows (per-element order check), lengths that are not multiples of 8 and data pointers that are
+# not 16-B aligned (element-wise staging), at the MFMA tile sizes
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("policy,ws,ls,causal,seq_dims,mode,qs,ks,misalign", [
+    ("local", 20, 2, False, 1, "none_front", (520,), (520,), False),
+    ("local", 9, 1, True, 1, "scale_front", (300,), (600,), False),
+    ("local", 5, 0, False, 2, "none_front", (24, 20), (24, 20), False),
+    ("local", 3, 1, True, 2, "scale_end", (16, 24), (20, 12), False),
+    ("full", 1, 0, False, 1, "none_front", (263,), (517,), False),
+    ("causal", 1, 0, False, 1, "scale_end", (333,), (199,), False),
+    ("local", 45, 0, False, 1, "none_front", (301,), (301,), False),
+    ("full", 1, 0, False, 1, "none_front", (256,), (192,), True),
+    ("local", 7, 1, False, 2, "scale_front", (15, 17), (13, 19), True),
+])
+def test_f16_fast_bwd_general(d, policy, ws, ls, causal, seq_dims, mode, qs, ks, misalign):
+    run_case(np.float16, policy, seq_dims, mode, (2, 2), d, d, qs, ks, ws=ws, ls=ls, causal=causal, seed=d + ws + ls,
+             misalign=misalign)
 
 
 # channel counts below the kernel's D (zero-padded rows) and d != v_d on the streamlined paths

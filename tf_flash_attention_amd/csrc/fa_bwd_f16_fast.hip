@@ -1,7 +1,8 @@
-// fa_bwd_f16_fast.hip — fp16 fused attention backward on gfx950 MFMA for the
-// common shapes (32 < max(d, v_d) <= 128, channels zero-padded to D ∈ {64, 128};
-// 16-byte aligned rows, nq % 8 == nk % 8 == 0)
-// under the full policy and the interval rules (causal, 1d unit-stride local).
+// fa_bwd_f16_fast.hip — fp16 fused attention backward on gfx950 MFMA for every rule
+// (full, causal, local in 1d/2d with any stride) and max(d, v_d) <= 128 (channels
+// zero-padded to D ∈ {64, 128}).  Rows whose 16-B chunks are aligned (16-B aligned
+// tensors, nq % 8 == nk % 8 == 0) stage with one 16-B buffer load per chunk; any other
+// length or alignment (ALN = false) loads the same chunks element by element.
 //
 // Replaces the reference's BackwardImpl (flash_attention.cu:1079-1967), which ran
 // every (key block, query block) pair as scalar SIMT GEMMs and serialised the dQ
@@ -22,8 +23,9 @@
 // against the algorithmic 10d) in exchange for writing dQ exactly once; the
 // single-kernel alternative (fa_bwd_f16.hip) spends that in fp32 atomics, which
 // cap it at ≈ 1.3 TB/s of added bytes (MI355X_MICROARCH.md 'Global float atomics').
-// Masks are rules (fa_rules.h): per-lane index intervals and per-wave tile classes;
-// tiles with no allowed pair are skipped.
+// Masks are rules (fa_rules.h): per-lane index intervals (POL 1: full windows of an
+// interval rule) or the per-element order check (POL 2: strided / 2d local windows), and
+// per-wave tile classes; tiles with no allowed pair are skipped.
 #include "fa_device.h"
 #include "fa_kernels.h"
 #include "fa_mfma.h"
@@ -99,7 +101,7 @@ struct DkdvSmem {
 // them behind).  One workgroup = NW waves x 32 keys of one (batch, head) slice.
 // ablation bits (timing diagnostics, outputs WRONG; FA_BWD_VARIANT=1300+bits, d = 128):
 // 1 no exp2, 2 no tile stores, 4 no tile loads, 8 no Q/dO transposed reads, 16 no G-image reads, 32 no barrier
-template <int D, int NW, int WPE, int POL, bool PIPE = false, int ABL = 0>
+template <int D, int NW, int WPE, int POL, bool ALN, bool PIPE = false, int ABL = 0>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -149,8 +151,11 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
       const int c = j / (kBK / 8), m = j % (kBK / 8);
       const bool in = c < (which ? vd : d) && k0 + 8 * m < nk;
-      rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? vrs2 : krs2,
-                                                     in ? (uint32_t)c * (uint32_t)nk * 2u + 16u * m : 0x80000000u, 2 * k0, 0);
+      if constexpr (ALN)
+        rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? vrs2 : krs2,
+                                                       in ? (uint32_t)c * (uint32_t)nk * 2u + 16u * m : 0x80000000u, 2 * k0, 0);
+      else
+        rv[jj] = buf_load8h(which ? vrs2 : krs2, (uint32_t)c * (uint32_t)nk * 2u, k0 + 8 * m, nk, c < (which ? vd : d));
     }
 #pragma unroll
     for (int jj = 0; jj < kRPT; ++jj) {
@@ -183,6 +188,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   const int key = k0 + 32 * w + r;
   const int wk0 = k0 + 32 * w;
   const bool wave_active = wk0 < nk;
+  const int ko = (POL == 2) ? seq_order(a.rule.k, a.rule, min(key, nk - 1)) : 0;  // this lane's key order
   int qlo = 0, qspan = nq, wlo_min = 0, wlo_max = 0, whi_min = nq - 1, whi_max = nq - 1;
   if (POL == 1 && wave_active) {
     int qhi;
@@ -199,6 +205,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
     const int qz = qa + 31;
     if (!wave_active) return 0;
     if (POL == 0) return 2;  // q >= nq rows carry lse2 = +inf -> P = 0; keys >= nk are never stored
+    if (POL == 2) return qa < nq ? tile_class(a.rule, qa, min(qz, nq - 1), wk0, min(wk0 + 31, nk - 1)) : 0;
     if (wlo_min > qz || whi_max < qa) return 0;
     return (wlo_max <= qa && whi_min >= qz) ? 2 : 1;
   };
@@ -211,7 +218,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
     const int idx = (tid + kThr * j) % kQChunks;
     crow_[j] = idx >> 2;
     cm_[j] = idx & 3;
-    voff[j] = (uint32_t)crow_[j] * (uint32_t)nq * 2u + 16u * cm_[j];
+    voff[j] = (uint32_t)crow_[j] * (uint32_t)nq * 2u + (ALN ? 16u * cm_[j] : 0u);  // (ALN: the chunk's; else the row's)
   }
   // two staging sets (tile t in set t&1): a tile is loaded two steps before it is stored
   u32x4 qr[2][kCPT];
@@ -224,8 +231,12 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) {
       const bool isO = is_o(j);
-      const bool out = qa + 8 * cm_[j] >= nq || crow_[j] >= (isO ? vd : d);
-      qr[set][j] = buf_load16(isO ? ors : qrs, voff[j], 2 * qa, out);
+      if constexpr (ALN) {
+        const bool out = qa + 8 * cm_[j] >= nq || crow_[j] >= (isO ? vd : d);
+        qr[set][j] = buf_load16(isO ? ors : qrs, voff[j], 2 * qa, out);
+      } else {
+        qr[set][j] = buf_load8h(isO ? ors : qrs, voff[j], qa + 8 * cm_[j], nq, crow_[j] < (isO ? vd : d));
+      }
     }
     if (tid < 64) {  // lanes 0..31: lse2, 32..63: D
       const int q = qa + (tid & 31);
@@ -319,6 +330,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       if (POL == 1 && cls == 1) {
         const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
         pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
+      }
+      if (POL == 2 && cls == 1) {
+        const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
+        pv = (q < nq && check_orders_bf(a.rule, seq_order(a.rule.q, a.rule, min(q, nq - 1)), ko)) ? pv : 0.f;
       }
       pf[i >> 3][i & 7] = (_Float16)pv;
       sf[i >> 3][i & 7] = (_Float16)(pv * pacc[i]);
@@ -478,7 +493,7 @@ struct DqSmem {
 };
 
 // dQ: query-outer.  One workgroup = NW waves x 32 queries of one (batch, head) slice.
-template <int D, int NW, int WPE, int POL, bool PRE = false>
+template <int D, int NW, int WPE, int POL, bool ALN, bool PRE = false>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -525,8 +540,11 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
       const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
       const int c = j / (kBM / 8), m = j % (kBM / 8);
       const bool in = c < (which ? vd : d) && q0 + 8 * m < nq;
-      rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? ors2 : qrs2,
-                                                     in ? (uint32_t)c * (uint32_t)nq * 2u + 16u * m : 0x80000000u, 2 * q0, 0);
+      if constexpr (ALN)
+        rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? ors2 : qrs2,
+                                                       in ? (uint32_t)c * (uint32_t)nq * 2u + 16u * m : 0x80000000u, 2 * q0, 0);
+      else
+        rv[jj] = buf_load8h(which ? ors2 : qrs2, (uint32_t)c * (uint32_t)nq * 2u, q0 + 8 * m, nq, c < (which ? vd : d));
     }
 #pragma unroll
     for (int jj = 0; jj < kRPT; ++jj) {
@@ -580,9 +598,16 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     const int kz = ka + kBN - 1;
     if (!wave_active) return 0;
     if (POL == 0) return kz < nk ? 2 : 1;
+    if (POL == 2) {  // class 2 only for tiles wholly inside nk (the staged tail past nk is masked)
+      if (ka >= nk) return 0;
+      const int c = tile_class(a.rule, wq0, min(wq0 + 31, nq - 1), ka, min(kz, nk - 1));
+      return (c == 2 && kz >= nk) ? 1 : c;
+    }
     if (wlo_min > kz || whi_max < ka) return 0;
     return (wlo_max <= ka && whi_min >= kz && kz < nk) ? 2 : 1;
   };
+
+  const int qo = (POL == 2) ? seq_order(a.rule.q, a.rule, min(qi, nq - 1)) : 0;  // this lane's query order
 
   // ---- key-tile staging (K, V chunks: 8 keys of one channel row)
   uint32_t voff[kCPT];
@@ -591,7 +616,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
   for (int j = 0; j < kCPT; ++j) {
     crow_[j] = ((tid + kThr * j) % kKChunks) >> 3;
-    voff[j] = (uint32_t)crow_[j] * (uint32_t)nk * 2u + 16u * cm;
+    voff[j] = (uint32_t)crow_[j] * (uint32_t)nk * 2u + (ALN ? 16u * cm : 0u);  // (ALN: the chunk's; else the row's)
   }
   // two staging sets (tile t in set t&1): a tile is loaded two steps before it is stored
   u32x4 kr[2][kCPT];
@@ -603,7 +628,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) {
       const bool isV = is_v(j);
-      kr[set][j] = buf_load16(isV ? vrs : krs, voff[j], 2 * min(ka, nk), out || crow_[j] >= (isV ? vd : d));
+      if constexpr (ALN)
+        kr[set][j] = buf_load16(isV ? vrs : krs, voff[j], 2 * min(ka, nk), out || crow_[j] >= (isV ? vd : d));
+      else
+        kr[set][j] = buf_load8h(isV ? vrs : krs, voff[j], ka + 8 * cm, nk, crow_[j] < (isV ? vd : d));
     }
   };
   auto store_tile = [&](int slot, int set) {
@@ -704,7 +732,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
         float pv = __builtin_amdgcn_exp2f(st[t][i]);
         if (cls == 1) {
           const int kk = ka + 32 * t + 16 * (i >> 3) + 8 * h + (i & 7);
-          const bool ok = (POL == 1) ? ((unsigned)(kk - klo) < (unsigned)kspan) : (kk < nk);
+          const bool ok = (POL == 1)   ? ((unsigned)(kk - klo) < (unsigned)kspan)
+                          : (POL == 2) ? (kk < nk && check_orders_bf(a.rule, qo, seq_order(a.rule.k, a.rule, min(kk, nk - 1))))
+                                       : (kk < nk);
           pv = ok ? pv : 0.f;
         }
         dsf[j] = (_Float16)(pv * dp[t][i]);
@@ -750,11 +780,29 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     }
 }
 
+// kernel POL from the rule: 0 full, 1 interval rules (causal, 1d unit-stride local), 2 any other local rule
+inline int bwd_pol(const Rule& r) { return r.policy == 0 ? 0 : rule_is_interval(r) ? 1 : 2; }
+// 16-B chunk staging: every tensor 16-B aligned and both lengths multiples of 8 (each channel row starts
+// on a 16-B boundary)
+inline bool bwd_aligned(const BwdArgs& a) {
+  const uintptr_t al = reinterpret_cast<uintptr_t>(a.Q) | reinterpret_cast<uintptr_t>(a.K) |
+                       reinterpret_cast<uintptr_t>(a.V) | reinterpret_cast<uintptr_t>(a.dO);
+  return (al % 16) == 0 && a.rule.q.n % 8 == 0 && a.rule.k.n % 8 == 0;
+}
+using BwdKernel = void (*)(BwdArgs);
+
 template <int D, int NW, int WPE, bool PIPE = false, int ABL = 0>
 hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
   using S = DkdvSmem<D, NW, PIPE ? 3 : 2>;
   const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
-  auto kern = a.rule.policy == 0 ? bwd_dkdv_kernel<D, NW, WPE, 0, PIPE, ABL> : bwd_dkdv_kernel<D, NW, WPE, 1, PIPE, ABL>;
+  const int pol = bwd_pol(a.rule);
+  const BwdKernel kern =
+      bwd_aligned(a) ? (pol == 0   ? bwd_dkdv_kernel<D, NW, WPE, 0, true, PIPE, ABL>
+                        : pol == 1 ? bwd_dkdv_kernel<D, NW, WPE, 1, true, PIPE, ABL>
+                                   : bwd_dkdv_kernel<D, NW, WPE, 2, true, PIPE, ABL>)
+                     : (pol == 0   ? bwd_dkdv_kernel<D, NW, WPE, 0, false, PIPE, ABL>
+                        : pol == 1 ? bwd_dkdv_kernel<D, NW, WPE, 1, false, PIPE, ABL>
+                                   : bwd_dkdv_kernel<D, NW, WPE, 2, false, PIPE, ABL>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(NW * 64), S::kTotal, s, a);
@@ -765,7 +813,13 @@ template <int D, int NW, int WPE, bool PRE = false>
 hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
   using S = DqSmem<D, NW>;
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
-  auto kern = a.rule.policy == 0 ? bwd_dq_kernel<D, NW, WPE, 0, PRE> : bwd_dq_kernel<D, NW, WPE, 1, PRE>;
+  const int pol = bwd_pol(a.rule);
+  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, true, PRE>
+                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, true, PRE>
+                                                      : bwd_dq_kernel<D, NW, WPE, 2, true, PRE>)
+                                        : (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, false, PRE>
+                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, false, PRE>
+                                                      : bwd_dq_kernel<D, NW, WPE, 2, false, PRE>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(NW * 64), S::kTotal, s, a);
@@ -776,12 +830,12 @@ hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
 
 bool bwd_f16_fast_supported(const BwdArgs& a) {
   const int nq = a.rule.q.n, nk = a.rule.k.n;
-  const uintptr_t al = reinterpret_cast<uintptr_t>(a.Q) | reinterpret_cast<uintptr_t>(a.K) |
-                       reinterpret_cast<uintptr_t>(a.V) | reinterpret_cast<uintptr_t>(a.dO);
   const int dm = max(a.d, a.v_d);
-  return dm > 32 && dm <= 128 && nq > 0 && nk > 0 && nq % 8 == 0 && nk % 8 == 0 &&
-         (al % 16) == 0 && (int64_t)dm * nq * 2 < (1ll << 31) && (int64_t)dm * nk * 2 < (1ll << 31) &&
-         rule_is_interval(a.rule) && a.b * ((nk + 127) / 128) < (1ll << 31) && a.b * ((nq + 127) / 128) < (1ll << 31);
+  // (buffer offsets are 32-bit: a channel row set of one slice stays below 2^31 bytes; the element-wise
+  // staging of the unaligned form addresses up to 2·n + 14 bytes past a row start)
+  return dm >= 1 && dm <= 128 && nq > 0 && nk > 0 && (int64_t)dm * (nq + 8) * 2 < (1ll << 31) &&
+         (int64_t)dm * (nk + 8) * 2 < (1ll << 31) && a.b * ((nk + 127) / 128) < (1ll << 31) &&
+         a.b * ((nq + 127) / 128) < (1ll << 31);
 }
 
 hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {

@@ -68,6 +68,18 @@ __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t rs, uint32_t 
   return __builtin_amdgcn_raw_buffer_load_b128(rs, out ? 0x80000000u : voff, soff, 0);
 }
 
+// 8 consecutive fp16 elements e..e+7 of the buffer row at byte offset `vrow`, any alignment (one
+// 2-B load each): elements at or past n, or of a row that is out of range, read as zeros
+__device__ __forceinline__ u32x4 buf_load8h(__amdgpu_buffer_rsrc_t rs, uint32_t vrow, int e, int n, bool rowok) {
+  uint32_t hh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool in = rowok && e + j < n;
+    hh[j] = __builtin_amdgcn_raw_buffer_load_b16(rs, in ? vrow + 2u * (uint32_t)(e + j) : 0x80000000u, 0, 0);
+  }
+  return u32x4{hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16)};
+}
+
 // 8 consecutive halfs starting at element e of a row of length n (zeros past n)
 __device__ __forceinline__ u32x4 load_chunk8(const __half* row, int e, int n, bool vec) {
   if (vec) return (e < n) ? *reinterpret_cast<const u32x4*>(row + e) : u32x4{0, 0, 0, 0};
