@@ -8,7 +8,8 @@
 // every (key block, query block) pair as scalar SIMT GEMMs and serialised the dQ
 // read-modify-write through a global spin lock.  Here the pass is split the way
 // the data wants to flow on this chip — no atomics, no locks, no dQ workspace:
-//   prep : D = rowsum(dO∘O), lse2 = m·log2e + log2 l                (per query)
+//   prep : -D = -rowsum(dO∘O), -lse2 = -(m·log2e + log2 l)            (per query, negated:
+//          the C operands of the S / dP chains)
 //   dkdv : key-outer.  A wave owns 32 keys; K·scale·log2e and V stay in registers
 //          as MFMA B operands, dK and dV accumulate in registers, and the query
 //          tiles (Q, dO, lse2, D) stream through a 2-slot LDS ring:
@@ -40,7 +41,8 @@ using namespace mf;
 constexpr int kThrPrep = 256;
 
 // ---------------------------------------------------------------------------
-// prep: D = rowsum(dO∘O) (fp32), lse2 = m*log2e + log2(l) (+inf if the row attends nothing)
+// prep: -D = -rowsum(dO∘O) (fp32), -lse2 = -(m*log2e + log2(l)) (-inf if the row attends nothing),
+// stored negated: both passes start their S / dP accumulator chains from them
 __global__ __launch_bounds__(kThrPrep) void bwd_prep_kernel(BwdArgs a) {
   const int nq = a.rule.q.n, vd = a.v_d;
   const int64_t total = a.b * (int64_t)nq;
@@ -59,8 +61,8 @@ __global__ __launch_bounds__(kThrPrep) void bwd_prep_kernel(BwdArgs a) {
   if (v < vd) D0 += __half2float(O[(int64_t)v * nq]) * __half2float(dO[(int64_t)v * nq]);
   const float l = static_cast<const float*>(a.l)[i];
   const float m = __half2float(static_cast<const __half*>(a.m)[i]);
-  static_cast<float*>(a.ws_D)[i] = D0 + D1;
-  static_cast<float*>(a.ws_lse)[i] = (l > 0.f) ? m * kLog2e + __log2f(l) : __builtin_huge_valf();
+  static_cast<float*>(a.ws_D)[i] = -(D0 + D1);
+  static_cast<float*>(a.ws_lse)[i] = (l > 0.f) ? -(m * kLog2e + __log2f(l)) : -__builtin_huge_valf();
 }
 
 // ---------------------------------------------------------------------------
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   auto tcls = [&](int qa) -> int {
     const int qz = qa + 31;
     if (!wave_active) return 0;
-    if (POL == 0) return 2;  // q >= nq rows carry lse2 = +inf -> P = 0; keys >= nk are never stored
+    if (POL == 0) return 2;  // q >= nq rows carry -lse2 = -inf -> P = 0; keys >= nk are never stored
     if (POL == 2) return qa < nq ? tile_class(a.rule, qa, min(qz, nq - 1), wk0, min(wk0 + 31, nk - 1)) : 0;
     if (wlo_min > qz || whi_max < qa) return 0;
     return (wlo_max <= qa && whi_min >= qz) ? 2 : 1;
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
     }
     if (tid < 64) {  // lanes 0..31: lse2, 32..63: D
       const int q = qa + (tid & 31);
-      lr[set] = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? __builtin_huge_valf() : 0.f);
+      lr[set] = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? -__builtin_huge_valf() : 0.f);
     }
   };
   auto store_tile = [&](int slot, int set) {
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) { dk[u][i] = 0.f; dv[u][i] = 0.f; }
 
-  // row constants of the tile in `base` as initial accumulators: S: -lse2[q], dP: -D[q]
+  // row constants of the tile in `base` (stored negated) as initial accumulators: S: -lse2[q], dP: -D[q]
   auto init_acc = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) {
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq) {  // registers 4gq..4gq+3 = queries 16(gq>>1) + 8h + 4(gq&1) + 0..3
@@ -269,8 +271,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       const floatx4 d4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 128 + 4 * q4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        sacc[4 * gq + j] = -l4[j];
-        pacc[4 * gq + j] = -d4[j];
+        sacc[4 * gq + j] = l4[j];
+        pacc[4 * gq + j] = d4[j];
       }
     }
   };
@@ -481,6 +483,351 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// dK / dV, producer / consumer (two waves per SIMD).  Waves w and w+4 share a SIMD and the same
+// 32 keys.  Wave w (producer) forms S = Qᵀ·K' and dP = dOᵀ·V for query tile i, P = exp2(S) and
+// dS = P∘dP, and hands P and dS to wave w+4 through LDS; wave w+4 (consumer) accumulates
+// dV += dO·P and dK += Q·dS for tile i-1.  The producer's softmax VALU runs beside the
+// consumer's MFMAs on the shared SIMD (the one-wave-per-SIMD kernel above serialises them), and
+// the register file splits along the data: K', V and the S / dP accumulators live in the
+// producer, the dK / dV accumulators in the consumer, each role inside its own loop so neither
+// carries the other's registers (under 256 each at D = 128).  Every step: one barrier, the
+// staging of tile i+1 into the ring, the load of tile i+3.
+template <int D>
+struct PcSmem {
+  static constexpr int kBK = 128;            // keys per workgroup: four producer waves x 32
+  static constexpr int kRow = D * kBK * 2;   // K (or V) row image (prologue only)
+  static constexpr int kQT = D * 64;         // one [D][32] Q16 image
+  static constexpr int offQT = 0, offOT = kQT, offLse = 2 * kQT;
+  static constexpr int kSlot = offLse + 2 * 32 * 4;  // + -lse2[32], -D[32]
+  static constexpr int kNS = 4;              // query-tile ring
+  static constexpr int offX = kNS * kSlot;   // P / dS hand-over: 2 slots x 4 waves x 4 KB
+  static constexpr int kXSlot = 4 * 4096;
+  static constexpr int kUsed = offX + 2 * kXSlot;
+  static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;  // the K/V images alias the ring
+};
+
+template <int D, int POL, bool ALN, int PF = 0>
+__global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char_t* smem = (lds_char_t*)smem_raw;
+  using S = PcSmem<D>;
+  constexpr int kThr = 512;
+  constexpr int kBK = S::kBK;
+  constexpr int kQChunks = D * 4;                 // 16-B chunks of one [D][32] tile
+  static_assert((2 * kQChunks) % kThr == 0, "tile chunks must divide over the workgroup");
+  constexpr int kCPT = 2 * kQChunks / kThr;       // Q and dO chunks per thread
+  // PF & 2: two barriers per step — phase A: the producer's S / dP MFMAs (the consumer stages and
+  // reads its operands), phase B: the producer's softmax beside the consumer's dV / dK MFMAs
+  constexpr bool TWO = (PF & 2) != 0;
+
+  const int nq = a.rule.q.n, nk = a.rule.k.n;
+  const uint32_t nkb = (nk + kBK - 1) / kBK;
+  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t bi = bid / nkb;
+  const int k0 = (int)(bid % nkb) * kBK;  // earliest (heaviest under causal) key blocks first
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = w >> 2, wl = w & 3;     // group 0 produces, group 1 consumes; wl: the key slice
+  const int h = lane >> 5, r = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const int sig = ((tp & 1) << 1) | (tp >> 1);  // (see the dK/dV kernel above: σ-permuted transposed reads)
+  const float c2 = (float)a.scale * kLog2e;
+
+  const int d = a.d, vd = a.v_d;
+  const __half* K = static_cast<const __half*>(a.K) + bi * (int64_t)d * nk;
+  const __half* V = static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk;
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq, 2u * d * nq);
+  const __amdgpu_buffer_rsrc_t ors = make_rsrc(static_cast<const __half*>(a.dO) + bi * (int64_t)vd * nq, 2u * vd * nq);
+  const float* glse = static_cast<const float*>(a.ws_lse) + bi * (int64_t)nq;
+  const float* gD = static_cast<const float*>(a.ws_D) + bi * (int64_t)nq;
+
+  // ---- K, V blocks into LDS (every thread); the producers read their resident B operands below
+  {
+    constexpr int kRPT = 2 * D * (kBK / 8) / kThr, kHalf = D * (kBK / 8) / kThr;
+    static_assert(kHalf * kThr == D * (kBK / 8), "resident chunks must divide over the workgroup");
+    const __amdgpu_buffer_rsrc_t krs2 = make_rsrc(K, 2u * d * nk), vrs2 = make_rsrc(V, 2u * vd * nk);
+    u32x4 rv[kRPT];
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
+      const int c = j / (kBK / 8), m = j % (kBK / 8);
+      const bool in = c < (which ? vd : d) && k0 + 8 * m < nk;
+      if constexpr (ALN)
+        rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? vrs2 : krs2,
+                                                       in ? (uint32_t)c * (uint32_t)nk * 2u + 16u * m : 0x80000000u, 2 * k0, 0);
+      else
+        rv[jj] = buf_load8h(which ? vrs2 : krs2, (uint32_t)c * (uint32_t)nk * 2u, k0 + 8 * m, nk, c < (which ? vd : d));
+    }
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
+      const int c = j / (kBK / 8), m = j % (kBK / 8);
+      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBK) + ((m * 16) ^ ((c & 3) << 6))) = rv[jj];
+    }
+  }
+  __syncthreads();
+
+  // ---- query range of this key block and the per-lane / per-wave query intervals (both roles)
+  const int klast = min(k0 + kBK, nk) - 1;
+  int qb = 0, qe = nq;
+  if (POL != 0) q_range_for_k_block(a.rule, k0, klast, &qb, &qe);
+  const int qt0 = (qb / 32) * 32;
+  const int ntiles = (qe > qb) ? (qe - qt0 + 31) / 32 : 0;
+  const int key = k0 + 32 * wl + r;
+  const int wk0 = k0 + 32 * wl;
+  const bool wave_active = wk0 < nk;
+  int qlo = 0, qspan = nq, wlo_min = 0, wlo_max = 0, whi_min = nq - 1, whi_max = nq - 1;
+  if (POL == 1 && wave_active) {
+    int qhi;
+    query_interval(a.rule, min(key, nk - 1), &qlo, &qhi);
+    qspan = max(qhi - qlo + 1, 0);
+    const int last = min(31, nk - 1 - wk0);
+    wlo_min = __builtin_amdgcn_readfirstlane(qlo);
+    whi_min = __builtin_amdgcn_readfirstlane(qhi);
+    wlo_max = __builtin_amdgcn_readlane(qlo, last);
+    whi_max = __builtin_amdgcn_readlane(qhi, last);
+  }
+  auto tcls = [&](int qa) -> int {
+    const int qz = qa + 31;
+    if (!wave_active) return 0;
+    if (POL == 0) return 2;  // q >= nq rows carry -lse2 = -inf -> P = 0; keys >= nk are never stored
+    if (POL == 2) return qa < nq ? tile_class(a.rule, qa, min(qz, nq - 1), wk0, min(wk0 + 31, nk - 1)) : 0;
+    if (wlo_min > qz || whi_max < qa) return 0;
+    return (wlo_max <= qa && whi_min >= qz) ? 2 : 1;
+  };
+
+  // ---- query-tile staging, every thread (Q, dO chunks: 8 queries of one channel row)
+  uint32_t voff[kCPT];
+  int crow_[kCPT], cm_[kCPT];
+#pragma unroll
+  for (int j = 0; j < kCPT; ++j) {
+    const int idx = (tid + kThr * j) % kQChunks;
+    crow_[j] = idx >> 2;
+    cm_[j] = idx & 3;
+    voff[j] = (uint32_t)crow_[j] * (uint32_t)nq * 2u + (ALN ? 16u * cm_[j] : 0u);
+  }
+  u32x4 qr[2][kCPT];  // two staging sets: tile t in set t&1, loaded two steps before it is stored
+  float lr[2] = {0.f, 0.f};
+  auto is_o = [&](int j) -> bool {
+    return (kQChunks % kThr == 0) ? (j >= kQChunks / kThr) : ((tid + kThr * j) >= kQChunks);
+  };
+  auto load_tile = [&](int qa, int set) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isO = is_o(j);
+      if constexpr (ALN) {
+        const bool out = qa + 8 * cm_[j] >= nq || crow_[j] >= (isO ? vd : d);
+        qr[set][j] = buf_load16(isO ? ors : qrs, voff[j], 2 * min(qa, nq), out);
+      } else {
+        qr[set][j] = buf_load8h(isO ? ors : qrs, voff[j], qa + 8 * cm_[j], nq, crow_[j] < (isO ? vd : d));
+      }
+    }
+    if (tid < 64) {  // lanes 0..31: -lse2, 32..63: -D
+      const int q = qa + (tid & 31);
+      lr[set] = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? -__builtin_huge_valf() : 0.f);
+    }
+  };
+  auto store_tile = [&](int slot, int set) __attribute__((always_inline)) {
+    lds_char_t* base = smem + slot * S::kSlot;
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isO = is_o(j);
+      *reinterpret_cast<lds_u32x4_t*>(base + (isO ? S::offOT : S::offQT) + q16_off(crow_[j], cm_[j])) = qr[set][j];
+    }
+    if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr[set];
+  };
+  // hand-over slot of this wave pair: four b128 per lane (P k-steps 0/1, dS k-steps 0/1), lane-linear
+  auto xoff = [&](int xs, int j) -> uint32_t { return S::offX + xs * S::kXSlot + wl * 4096 + j * 1024 + lane * 16; };
+
+  // Steps it = 0 .. ntiles: the producer handles tile it (it < ntiles), the consumer tile it-1 (it >= 1).
+  // Whole groups of four steps (ring slot it % 4, staging set (it+1) % 2, hand-over slot it % 2 are
+  // compile-time); loads and stores are unconditional (phantom tiles move zeros), so hipcc's vmcnt
+  // waits stay exact.
+  const int nsteps = ntiles + 1;
+  auto stage = [&](auto C_, int it) __attribute__((always_inline)) {
+    constexpr int c = decltype(C_)::value;
+    __syncthreads();
+    store_tile((c + 1) % 4, (c + 1) % 2);           // tile it+1 (loaded in step it-2)
+    load_tile(qt0 + 32 * (it + 3), (c + 1) % 2);    // tile it+3 into the set just stored
+  };
+  // first tiles: tile 0's loads issued now, its store after the barrier that retires the K/V images
+  load_tile(qt0, 0);
+  auto stage0 = [&]() __attribute__((always_inline)) {
+    __syncthreads();
+    store_tile(0, 0);
+    load_tile(qt0 + 32, 1);
+    load_tile(qt0 + 64, 0);
+  };
+
+  if (grp == 0) {
+    // ================= producer
+    half8 kb[D / 16], vb[D / 16];  // resident B operands: lane (r,h) holds X[c = 16s + 8h + j][key]
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int crow = 16 * s + 8 * (g >> 1) + 4 * e + tq;
+        const int col = 32 * wl + 16 * (g & 1) + 4 * tp;
+        const uint32_t off = crow * (2 * kBK) + ((col * 2) ^ ((crow & 3) << 6));
+        const half4 x = tr_read(smem + off), y = tr_read(smem + S::kRow + off);
+        if (e == 0) { kb[s].lo = x; vb[s].lo = y; } else { kb[s].hi = x; vb[s].hi = y; }
+      }
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) kb[s] = scale8(kb[s], c2);  // S in log2 units straight out of the MFMA
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every image read done before the ring reuses it
+    stage0();
+    const int ko = (POL == 2) ? seq_order(a.rule.k, a.rule, min(key, nk - 1)) : 0;
+    auto pstep = [&](auto C_, int it) __attribute__((always_inline)) {
+      constexpr int c = decltype(C_)::value;
+      stage(C_, it);
+      const int qa = qt0 + 32 * it;
+      const int cls = it < ntiles ? tcls(qa) : 0;
+      const lds_char_t* base = smem + c * S::kSlot;
+      floatx16 sacc, pacc;
+      if (cls != 0) {
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {  // registers 4gq..4gq+3 = queries 16(gq>>1) + 8h + 4(gq&1) + 0..3
+          const int q4 = 16 * (gq >> 1) + 8 * h + 4 * (gq & 1);
+          const floatx4 l4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 4 * q4);
+          const floatx4 d4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 128 + 4 * q4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            sacc[4 * gq + j] = l4[j];
+            pacc[4 * gq + j] = d4[j];
+          }
+        }
+        // S = Qᵀ·K', dP = dOᵀ·V: A operands by transposed reads, two k-steps ahead of their MFMAs
+        constexpr int kS = D / 16, kAh = 2;
+        half8 qa8[kAh + 1], oa8[kAh + 1];
+        auto rd = [&](int s_) __attribute__((always_inline)) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const uint32_t off = q16_off(16 * s_ + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
+            const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
+            if (e == 0) { qa8[s_ % (kAh + 1)].lo = x; oa8[s_ % (kAh + 1)].lo = y; }
+            else { qa8[s_ % (kAh + 1)].hi = x; oa8[s_ % (kAh + 1)].hi = y; }
+          }
+        };
+#pragma unroll
+        for (int s_ = 0; s_ < kAh; ++s_) rd(s_);
+        if constexpr ((PF & 1) != 0) __builtin_amdgcn_s_setprio(1);  // the S / dP MFMAs first; the consumer's fill in
+#pragma unroll
+        for (int s_ = 0; s_ < kS; ++s_) {
+          if (s_ + kAh < kS) rd(s_ + kAh);
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8[s_ % (kAh + 1)], kb[s_], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8[s_ % (kAh + 1)], vb[s_], pacc, 0, 0, 0);
+        }
+        if constexpr ((PF & 1) != 0) __builtin_amdgcn_s_setprio(0);
+      }
+      if constexpr (TWO) __builtin_amdgcn_s_barrier();  // phase B: this softmax beside the consumer's MFMAs
+      if (cls == 0) return;
+      // P = exp2(S), dS = P∘dP; register i = query 16(i>>3) + 8h + (i&7) = k-step i>>3 of the consumer
+      half8 pf[2], sf[2];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float pv = __builtin_amdgcn_exp2f(sacc[i]);
+        if (POL == 1 && cls == 1) {
+          const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
+          pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
+        }
+        if (POL == 2 && cls == 1) {
+          const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
+          pv = (q < nq && check_orders_bf(a.rule, seq_order(a.rule.q, a.rule, min(q, nq - 1)), ko)) ? pv : 0.f;
+        }
+        pf[i >> 3][i & 7] = (_Float16)pv;
+        sf[i >> 3][i & 7] = (_Float16)(pv * pacc[i]);
+      }
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) {
+        *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, s_)) = pf[s_];
+        *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, 2 + s_)) = sf[s_];
+      }
+    };
+    for (int it = 0; it < nsteps; it += 4) {
+      pstep(IC<0>{}, it);
+      pstep(IC<1>{}, it + 1);
+      pstep(IC<2>{}, it + 2);
+      pstep(IC<3>{}, it + 3);
+    }
+    return;
+  }
+
+  // ================= consumer
+  stage0();
+  floatx16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { dk[u][i] = 0.f; dv[u][i] = 0.f; }
+  auto cstep = [&](auto C_, int it) __attribute__((always_inline)) {
+    constexpr int c = decltype(C_)::value;
+    stage(C_, it);
+    const int qa = qt0 + 32 * (it - 1);
+    const int cls = (it >= 1 && it - 1 < ntiles) ? tcls(qa) : 0;
+    const lds_char_t* base = smem + ((c + 3) % 4) * S::kSlot;
+    // dV += dO·P, dK += Q·dS: A = X[row 32u + r][queries 16s + 8h + 0..7] (b128 reads, two ahead)
+    constexpr int kU = D / 32, kN = 2 * kU, kAh = 2;
+    half8 pf[2], sf[2], oa[kAh + 1], qa_[kAh + 1];
+    auto rd = [&](int n) __attribute__((always_inline)) {
+      const int s_ = n / kU, u = n % kU;
+      oa[n % (kAh + 1)] = read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s_ + h));
+      qa_[n % (kAh + 1)] = read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s_ + h));
+    };
+    if (cls != 0) {
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) {
+        pf[s_] = read_b128(smem + xoff((c + 1) % 2, s_));
+        sf[s_] = read_b128(smem + xoff((c + 1) % 2, 2 + s_));
+      }
+#pragma unroll
+      for (int n = 0; n < kAh; ++n) rd(n);
+    }
+    if constexpr (TWO) __builtin_amdgcn_s_barrier();  // phase B: these MFMAs beside the producer's softmax
+    if (cls == 0) return;
+#pragma unroll
+    for (int n = 0; n < kN; ++n) {
+      if (n + kAh < kN) rd(n + kAh);
+      const int s_ = n / kU, u = n % kU;
+      dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa[n % (kAh + 1)], pf[s_], dv[u], 0, 0, 0);
+      dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa_[n % (kAh + 1)], sf[s_], dk[u], 0, 0, 0);
+    }
+  };
+  for (int it = 0; it < nsteps; it += 4) {
+    cstep(IC<0>{}, it);
+    cstep(IC<1>{}, it + 1);
+    cstep(IC<2>{}, it + 2);
+    cstep(IC<3>{}, it + 3);
+  }
+
+  // ---- dK = scale·Σ dS·Q, dV: rows c = 32u + (i&3) + 8(i>>2) + 4h, column = this lane's key
+  if (!wave_active || key >= nk) return;
+  __half* dK = static_cast<__half*>(a.dK) + bi * (int64_t)d * nk;
+  __half* dV = static_cast<__half*>(a.dV) + bi * (int64_t)vd * nk;
+  const float sc = (float)a.scale;
+  if (d == D && vd == D) {
+    const __amdgpu_buffer_rsrc_t krs_ = make_rsrc(dK, 2u * d * nk), vrs_ = make_rsrc(dV, 2u * vd * nk);
+    const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nk + (uint32_t)key);
+#pragma unroll
+    for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t so = 2u * (32u * u + (i & 3) + 8u * (i >> 2)) * (uint32_t)nk;
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(dk[u][i] * sc)), krs_, vlane, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)dv[u][i]), vrs_, vlane, so, 0);
+      }
+    return;
+  }
+#pragma unroll
+  for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (c < d) dK[(int64_t)c * nk + key] = __float2half(dk[u][i] * sc);
+      if (c < vd) dV[(int64_t)c * nk + key] = __float2half(dv[u][i]);
+    }
+}
+
+// ---------------------------------------------------------------------------
 template <int D, int NW>
 struct DqSmem {
   static constexpr int kBM = 32 * NW;                 // queries per workgroup
@@ -572,7 +919,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   {
     const float* glse = static_cast<const float*>(a.ws_lse) + bi * (int64_t)nq;
     const float* gD = static_cast<const float*>(a.ws_D) + bi * (int64_t)nq;
-    const float lv = (qi < nq) ? -glse[qi] : kNegInf, dv = (qi < nq) ? -gD[qi] : 0.f;
+    const float lv = (qi < nq) ? glse[qi] : kNegInf, dv = (qi < nq) ? gD[qi] : 0.f;  // (stored negated)
 #pragma unroll
     for (int i = 0; i < 16; ++i) { negl[i] = lv; negd[i] = dv; }
   }
@@ -809,6 +1156,23 @@ hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int D, int PF = 0>
+hipError_t launch_dkdv_pc(const BwdArgs& a, hipStream_t s) {
+  using S = PcSmem<D>;
+  const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
+  const int pol = bwd_pol(a.rule);
+  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dkdv_pc_kernel<D, 0, true, PF>
+                                           : pol == 1 ? bwd_dkdv_pc_kernel<D, 1, true, PF>
+                                                      : bwd_dkdv_pc_kernel<D, 2, true, PF>)
+                                        : (pol == 0   ? bwd_dkdv_pc_kernel<D, 0, false, PF>
+                                           : pol == 1 ? bwd_dkdv_pc_kernel<D, 1, false, PF>
+                                                      : bwd_dkdv_pc_kernel<D, 2, false, PF>);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(512), S::kTotal, s, a);
+  return hipGetLastError();
+}
+
 template <int D, int NW, int WPE, bool PRE = false>
 hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
   using S = DqSmem<D, NW>;
@@ -844,7 +1208,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
 #ifdef FA_DIAG
-  // FA_BWD_VARIANT selects A/B structures (82, 1067-1069, 1200, 1264, 1267, 1281) and the
+  // FA_BWD_VARIANT selects A/B structures (82, 1067-1069, 1200, 1264, 1265, 1267, 1281, 1400-1403) and the
   // d = 128 dK/dV ablations 1301-1363 (outputs WRONG)
   const int v = diag_variant("FA_BWD_VARIANT");
   if (max(a.d, a.v_d) <= 64 && v >= 0) {
@@ -862,6 +1226,11 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   }
   if (max(a.d, a.v_d) > 64 && v >= 0) {
     switch (v) {
+      case 1400: e = launch_dkdv_pc<128>(a, s); break;
+      case 1265: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;  // round-2 default (one wave per SIMD)
+      case 1401: e = launch_dkdv_pc<128, 1>(a, s); break;
+      case 1402: e = launch_dkdv_pc<128, 2>(a, s); break;
+      case 1403: e = launch_dkdv_pc<128, 3>(a, s); break;
       case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
       case 1200: e = launch_dkdv<128, 4, 1>(a, s); break;  // operand reads not run ahead (before the default)
       case 1264: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
@@ -874,7 +1243,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
       case 1324: e = launch_dkdv<128, 4, 1, false, 24>(a, s); break;
       case 1338: e = launch_dkdv<128, 4, 1, false, 38>(a, s); break;
       case 1363: e = launch_dkdv<128, 4, 1, false, 63>(a, s); break;
-      default: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
+      default: e = launch_dkdv_pc<128>(a, s); break;
     }
     if (e != hipSuccess) return e;
     if (v == 1200 || v == 1264) return launch_dq<128, 4, 1>(a, s);
@@ -886,8 +1255,10 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
     if (e != hipSuccess) return e;
     return launch_dq<64, 4, 2>(a, s);
   }
-  // tuned (c3): operand reads two MFMA pairs ahead in both passes (10.97 -> 9.93 ms backward)
-  e = launch_dkdv<128, 4, 1, false, 64>(a, s);
+  // tuned (c3): the producer / consumer dK/dV pass (one-process A/B: 9.20 -> 8.59 ms backward; two
+  // barriers per step, 1402, and a prioritised producer, 1401, measured 8.70 / 8.77), operand reads
+  // two MFMA pairs ahead in the dQ pass (10.97 -> 9.93 ms backward before)
+  e = launch_dkdv_pc<128>(a, s);
   if (e != hipSuccess) return e;
   return launch_dq<128, 4, 1, true>(a, s);
 }
