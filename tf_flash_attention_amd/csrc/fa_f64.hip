@@ -19,6 +19,10 @@
 //   prep    : D = rowsum(dO∘O), lse = m + log l (+inf for empty rows)
 //   dkdv    : key-outer, K·scale and V resident; S = Qᵀ·K' (C = -lse), dP = dOᵀ·V (C = -D)
 //   dq      : query-outer, Q·scale and dO resident; Sᵀ = Kᵀ·Q', dPᵀ = Vᵀ·dO, dQ += K·dSᵀ
+// At 64 < D <= 128 the backward streams 16-column tiles (the two-slot ring of the Q/dO row and
+// transposed images then fits LDS) and the dK/dV pass runs twice, each launch accumulating one
+// half of the channels (the resident K', V operands plus all 128 channels of dK and dV would not
+// fit two waves per SIMD): the S / dP products are formed in both launches.
 // Row images ([channel][32 keys|queries]) swap their 16-column halves on odd
 // channel rows so the four lane groups of an A-operand read hit disjoint banks;
 // transposed images ([32][D+16]) are padded for the same reason.
@@ -52,8 +56,13 @@ __device__ __forceinline__ double grp_sum(double x) {
   x += __shfl_xor(x, 16);
   return x + __shfl_xor(x, 32);
 }
-// row image index: [c][32] with the 16-column halves swapped on odd rows
-__device__ __forceinline__ int rimg(int c, int col) { return c * kT + (col ^ ((c & 1) << 4)); }
+// row image index: [c][TT] — at TT = 32 with the 16-column halves swapped on odd rows (a 256-B
+// row puts the four lane groups' rows of an A read on the same banks otherwise); 128-B rows
+// (TT = 16) already fall in alternate bank halves
+template <int TT = kT>
+__device__ __forceinline__ int rimg(int c, int col) {
+  return TT == 32 ? c * TT + (col ^ ((c & 1) << 4)) : c * TT + col;
+}
 // doubles row[e], row[e+1] (zeros past n)
 __device__ __forceinline__ doublex2 load2(const double* row, int e, int n, bool vec) {
   if (vec && e + 2 <= n) return *reinterpret_cast<const doublex2*>(row + e);
@@ -69,14 +78,15 @@ __device__ __forceinline__ bool vec_ok(int n, const void* p0, const void* p1) {
 // Streams tensors A [da][n] and B [db][n] in kT-column tiles: row image of A, row image
 // of B (kRB), transposed images ([kT][D+16]) of A (kTA) and B (kTB).  Register-staged
 // one tile ahead.
-template <int D, bool kRB, bool kTA, bool kTB>
+template <int D, bool kRB, bool kTA, bool kTB, int TT = kT>
 struct Stream64 {
   static constexpr int kP = D + 16;
-  static constexpr int offA = 0, offB = D * kT, offAT = offB + (kRB ? D * kT : 0);
-  static constexpr int offBT = offAT + (kTA ? kT * kP : 0);
-  static constexpr int offC = offBT + (kTB ? kT * kP : 0);
-  static constexpr int kSlot = offC + 2 * kT;         // doubles (+ two kT row-constant vectors)
-  static constexpr int kChunks = D * (kT / 2);        // double2 chunks per tensor
+  static constexpr int offA = 0, offB = D * TT, offAT = offB + (kRB ? D * TT : 0);
+  static constexpr int offBT = offAT + (kTA ? TT * kP : 0);
+  static constexpr int offC = offBT + (kTB ? TT * kP : 0);
+  static constexpr int kSlot = offC + 2 * TT;         // doubles (+ two TT row-constant vectors)
+  static constexpr int kCR = TT / 2;                  // double2 chunks per row
+  static constexpr int kChunks = D * kCR;             // double2 chunks per tensor
   static constexpr int kCPT = (2 * kChunks + kThr - 1) / kThr;
   const double* A;
   const double* B;
@@ -90,7 +100,7 @@ struct Stream64 {
       doublex2 v = {0.0, 0.0};
       if (idx < 2 * kChunks) {
         const bool isB = idx >= kChunks;
-        const int k = isB ? idx - kChunks : idx, c = k >> 4, m = k & 15;
+        const int k = isB ? idx - kChunks : idx, c = k / kCR, m = k % kCR;
         if (c < (isB ? db : da)) v = load2((isB ? B : A) + (int64_t)c * n, col0 + 2 * m, n, vec);
       }
       reg[j] = v;
@@ -102,8 +112,8 @@ struct Stream64 {
       const int idx = threadIdx.x + kThr * j;
       if (idx < 2 * kChunks) {
         const bool isB = idx >= kChunks;
-        const int k = isB ? idx - kChunks : idx, c = k >> 4, m = k & 15;
-        if (!isB || kRB) *reinterpret_cast<lds_d2_t*>(slot + (isB ? offB : offA) + rimg(c, 2 * m)) = reg[j];
+        const int k = isB ? idx - kChunks : idx, c = k / kCR, m = k % kCR;
+        if (!isB || kRB) *reinterpret_cast<lds_d2_t*>(slot + (isB ? offB : offA) + rimg<TT>(c, 2 * m)) = reg[j];
         if (isB ? kTB : kTA) {
           lds_d_t* tr = slot + (isB ? offBT : offAT);
           tr[(2 * m) * kP + c] = reg[j][0];
@@ -305,18 +315,52 @@ __global__ __launch_bounds__(kThrPrep) void bwd_prep_f64_kernel(BwdArgs a) {
   static_cast<double*>(a.ws_lse)[i] = (l > 0.0) ? m + log(l) : __builtin_huge_val();
 }
 
-template <int D>
+// D <= 64: the resident K and V (Q and dO) blocks are staged together; at D = 128 one after the other
+template <int D, int TT>
 constexpr int bwd64_smem() {
-  constexpr int s1 = 2 * Stream64<D, true, true, true>::kSlot, s2 = 2 * D * kBM;
+  constexpr int s1 = 2 * Stream64<D, true, true, true, TT>::kSlot, s2 = (D > 64 ? 1 : 2) * D * kBM;
   return 8 * (s1 > s2 ? s1 : s2);
 }
 
-// dK / dV: 8 waves x 16 keys; query tiles of 32 (Q, dO row + transposed images, lse, D)
-template <int D, int POL>
+// resident B operands X[c = 4s + g][col0 + 16w + r] (x scale) of two tensors, through LDS: both images
+// at once for D <= 64, one at a time above (a [128][128] double image is 128 KB)
+template <int D>
+__device__ __forceinline__ void resident_pair(lds_d_t* smem, const double* X, int dx, const double* Y, int dy, int n,
+                                              int col0, bool vec, double xs, double (&xf)[D / 4], double (&yf)[D / 4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+  if constexpr (D <= 64) {
+    stage_block<D>(smem, X, dx, n, col0, vec);
+    stage_block<D>(smem + D * kBM, Y, dy, n, col0, vec);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < D / 4; ++s) {
+      xf[s] = smem[(4 * s + g) * kBM + 16 * w + r] * xs;
+      yf[s] = smem[D * kBM + (4 * s + g) * kBM + 16 * w + r];
+    }
+  } else {
+    stage_block<D>(smem, X, dx, n, col0, vec);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < D / 4; ++s) xf[s] = smem[(4 * s + g) * kBM + 16 * w + r] * xs;
+    __syncthreads();
+    stage_block<D>(smem, Y, dy, n, col0, vec);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < D / 4; ++s) yf[s] = smem[(4 * s + g) * kBM + 16 * w + r];
+  }
+  __syncthreads();
+}
+
+// dK / dV: 8 waves x 16 keys; query tiles of TT (Q, dO row + transposed images, lse, D).
+// CH < 0: every channel of dK / dV; CH = 0 / 1: channels [CH·D/2, CH·D/2 + D/2) only
+template <int D, int POL, int TT = kT, int CH = -1>
 __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_d_t* smem = (lds_d_t*)smem_raw;
-  using St = Stream64<D, true, true, true>;
+  using St = Stream64<D, true, true, true, TT>;
+  constexpr int kNT = TT / 16;                      // 16-query blocks per tile
+  constexpr int kNU = (CH < 0 ? D : D / 2) / 16;    // 16-channel blocks of dK / dV held
+  constexpr int kC0 = CH < 0 ? 0 : CH * (D / 2);    // first channel held
   const int nq = a.rule.q.n, nk = a.rule.k.n, d = a.d, vd = a.v_d;
   const uint32_t nkb = (nk + kBM - 1) / kBM;
   const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -331,23 +375,14 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
   const double* glse = static_cast<const double*>(a.ws_lse) + bi * (int64_t)nq;
   const double* gD = static_cast<const double*>(a.ws_D) + bi * (int64_t)nq;
 
-  const bool kvec = vec_ok(nk, a.K, a.V);
-  stage_block<D>(smem, K, d, nk, k0, kvec);
-  stage_block<D>(smem + D * kBM, V, vd, nk, k0, kvec);
-  __syncthreads();
   double kb[D / 4], vb[D / 4];  // B operands: X[c = 4s + g][key = k0 + 16w + r]
-#pragma unroll
-  for (int s = 0; s < D / 4; ++s) {
-    kb[s] = smem[(4 * s + g) * kBM + 16 * w + r] * sc;
-    vb[s] = smem[D * kBM + (4 * s + g) * kBM + 16 * w + r];
-  }
-  __syncthreads();
+  resident_pair<D>(smem, K, d, V, vd, nk, k0, vec_ok(nk, a.K, a.V), sc, kb, vb);
 
   const int klast = min(k0 + kBM, nk) - 1;
   int qb = 0, qe = nq;
   if (POL != 0) q_range_for_k_block(a.rule, k0, klast, &qb, &qe);
-  const int qt0 = (qb / kT) * kT;
-  const int ntiles = (qe > qb) ? (qe - qt0 + kT - 1) / kT : 0;
+  const int qt0 = (qb / TT) * TT;
+  const int ntiles = (qe > qb) ? (qe - qt0 + TT - 1) / TT : 0;
   const int wk0 = k0 + 16 * w, wk1 = min(wk0 + 15, nk - 1);
   const int key = wk0 + r;
   const bool wave_active = wk0 < nk;
@@ -364,53 +399,53 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
   double cr = 0.0;
   auto load_tile = [&](int qa) {
     st.load(qa);
-    if (tid < 2 * kT) {
-      const int q = qa + (tid & (kT - 1));
-      cr = (q < nq) ? ((tid < kT) ? glse[q] : gD[q]) : ((tid < kT) ? __builtin_huge_val() : 0.0);
+    if (tid < 2 * TT) {
+      const int q = qa + (tid & (TT - 1));
+      cr = (q < nq) ? ((tid < TT) ? glse[q] : gD[q]) : ((tid < TT) ? __builtin_huge_val() : 0.0);
     }
   };
   auto store_tile = [&](int slot) {
     lds_d_t* b = smem + slot * St::kSlot;
     st.store(b);
-    if (tid < 2 * kT) b[St::offC + tid] = cr;
+    if (tid < 2 * TT) b[St::offC + tid] = cr;
   };
 
-  doublex4 dk[D / 16], dv[D / 16];
+  doublex4 dk[kNU], dv[kNU];
 #pragma unroll
-  for (int u = 0; u < D / 16; ++u) dk[u] = dv[u] = splat4(0.0);
+  for (int u = 0; u < kNU; ++u) dk[u] = dv[u] = splat4(0.0);
 
   if (ntiles > 0) { load_tile(qt0); store_tile(0); }
-  if (ntiles > 1) load_tile(qt0 + kT);
+  if (ntiles > 1) load_tile(qt0 + TT);
   for (int it = 0; it < ntiles; ++it) {
     __syncthreads();
-    const int qa = qt0 + it * kT;
+    const int qa = qt0 + it * TT;
     if (it + 1 < ntiles) store_tile((it + 1) & 1);
-    if (it + 2 < ntiles) load_tile(qa + 2 * kT);
+    if (it + 2 < ntiles) load_tile(qa + 2 * TT);
     int cls = 2;
     if (!wave_active) cls = 0;
-    else if (POL != 0) cls = tile_class(a.rule, qa, min(qa + kT, nq) - 1, wk0, wk1);
+    else if (POL != 0) cls = tile_class(a.rule, qa, min(qa + TT, nq) - 1, wk0, wk1);
     if (cls == 0) continue;
     const lds_d_t* base = smem + (it & 1) * St::kSlot;
-    doublex4 sacc[2], pacc[2];
+    doublex4 sacc[kNT], pacc[kNT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < kNT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ql = 16 * t + g + 4 * i;
         sacc[t][i] = -base[St::offC + ql];
-        pacc[t][i] = -base[St::offC + kT + ql];
+        pacc[t][i] = -base[St::offC + TT + ql];
       }
     // S = Qᵀ·K', dP = dOᵀ·V: A = X[c = 4s + g][q = 16t + r] from the row images
 #pragma unroll
     for (int s = 0; s < D / 4; ++s)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        sacc[t] = mma(base[St::offA + rimg(4 * s + g, 16 * t + r)], kb[s], sacc[t]);
-        pacc[t] = mma(base[St::offB + rimg(4 * s + g, 16 * t + r)], vb[s], pacc[t]);
+      for (int t = 0; t < kNT; ++t) {
+        sacc[t] = mma(base[St::offA + rimg<TT>(4 * s + g, 16 * t + r)], kb[s], sacc[t]);
+        pacc[t] = mma(base[St::offB + rimg<TT>(4 * s + g, 16 * t + r)], vb[s], pacc[t]);
       }
-    double p[2][4], ds[2][4];
+    double p[kNT][4], ds[kNT][4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < kNT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         double pv = exp(sacc[t][i]);
@@ -426,14 +461,14 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
       }
     // dV += dO·P, dK += Q·dS: k-step (t, i) = queries 16t + 4i + g (transposed images)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < kNT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ql = 16 * t + 4 * i + g;
 #pragma unroll
-        for (int u = 0; u < D / 16; ++u) {
-          dv[u] = mma(base[St::offBT + ql * St::kP + 16 * u + r], p[t][i], dv[u]);
-          dk[u] = mma(base[St::offAT + ql * St::kP + 16 * u + r], ds[t][i], dk[u]);
+        for (int u = 0; u < kNU; ++u) {
+          dv[u] = mma(base[St::offBT + ql * St::kP + kC0 + 16 * u + r], p[t][i], dv[u]);
+          dk[u] = mma(base[St::offAT + ql * St::kP + kC0 + 16 * u + r], ds[t][i], dk[u]);
         }
       }
   }
@@ -442,21 +477,22 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
   double* dK = static_cast<double*>(a.dK) + bi * (int64_t)d * nk;
   double* dV = static_cast<double*>(a.dV) + bi * (int64_t)vd * nk;
 #pragma unroll
-  for (int u = 0; u < D / 16; ++u)
+  for (int u = 0; u < kNU; ++u)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = 16 * u + g + 4 * i;
+      const int c = kC0 + 16 * u + g + 4 * i;
       if (c < d) dK[(int64_t)c * nk + key] = dk[u][i] * sc;
       if (c < vd) dV[(int64_t)c * nk + key] = dv[u][i];
     }
 }
 
-// dQ: 8 waves x 16 queries; key tiles of 32 (K, V row images + K transposed image)
-template <int D, int POL>
+// dQ: 8 waves x 16 queries; key tiles of TT (K, V row images + K transposed image)
+template <int D, int POL, int TT = kT>
 __global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_d_t* smem = (lds_d_t*)smem_raw;
-  using St = Stream64<D, true, true, false>;
+  using St = Stream64<D, true, true, false, TT>;
+  constexpr int kNT = TT / 16;  // 16-key blocks per tile
   const double kNegInf = -__builtin_huge_val();
   const int nq = a.rule.q.n, nk = a.rule.k.n, d = a.d, vd = a.v_d;
   const uint32_t nqb = (nq + kBM - 1) / kBM;
@@ -470,17 +506,8 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
   const double* Q = static_cast<const double*>(a.Q) + bi * (int64_t)d * nq;
   const double* dO = static_cast<const double*>(a.dO) + bi * (int64_t)vd * nq;
 
-  const bool qvec = vec_ok(nq, a.Q, a.dO);
-  stage_block<D>(smem, Q, d, nq, q0, qvec);
-  stage_block<D>(smem + D * kBM, dO, vd, nq, q0, qvec);
-  __syncthreads();
   double qf[D / 4], of[D / 4];  // B operands: X[c = 4s + g][q = q0 + 16w + r]
-#pragma unroll
-  for (int s = 0; s < D / 4; ++s) {
-    qf[s] = smem[(4 * s + g) * kBM + 16 * w + r] * sc;
-    of[s] = smem[D * kBM + (4 * s + g) * kBM + 16 * w + r];
-  }
-  __syncthreads();
+  resident_pair<D>(smem, Q, d, dO, vd, nq, q0, vec_ok(nq, a.Q, a.dO), sc, qf, of);
 
   const int wq0 = q0 + 16 * w, wq1 = min(wq0 + 15, nq - 1);
   const int qi = wq0 + r;
@@ -495,8 +522,8 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
   const int qlast = min(q0 + kBM, nq) - 1;
   int kb = 0, ke = nk;
   if (POL != 0) k_range_for_q_block(a.rule, q0, qlast, &kb, &ke);
-  const int kt0 = (kb / kT) * kT;
-  const int ntiles = (ke > kb) ? (ke - kt0 + kT - 1) / kT : 0;
+  const int kt0 = (kb / TT) * TT;
+  const int ntiles = (ke > kb) ? (ke - kt0 + TT - 1) / TT : 0;
   const int qo = (POL == 2) ? seq_order(a.rule.q, a.rule, min(qi, nq - 1)) : 0;
   int klo = 0, kspan = nk;
   if (POL == 1 && wave_active) {
@@ -512,34 +539,37 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
   for (int u = 0; u < D / 16; ++u) dq[u] = splat4(0.0);
 
   if (ntiles > 0) { st.load(kt0); st.store(smem); }
-  if (ntiles > 1) st.load(kt0 + kT);
+  if (ntiles > 1) st.load(kt0 + TT);
   for (int it = 0; it < ntiles; ++it) {
     __syncthreads();
-    const int ka = kt0 + it * kT;
+    const int ka = kt0 + it * TT;
     if (it + 1 < ntiles) st.store(smem + ((it + 1) & 1) * St::kSlot);
-    if (it + 2 < ntiles) st.load(ka + 2 * kT);
+    if (it + 2 < ntiles) st.load(ka + 2 * TT);
     int cls;
     if (!wave_active) cls = 0;
-    else if (POL == 0) cls = (ka + kT <= nk) ? 2 : 1;
+    else if (POL == 0) cls = (ka + TT <= nk) ? 2 : 1;
     else {
-      cls = tile_class(a.rule, wq0, wq1, ka, min(ka + kT, nk) - 1);
-      if (cls == 2 && ka + kT > nk) cls = 1;
+      cls = tile_class(a.rule, wq0, wq1, ka, min(ka + TT, nk) - 1);
+      if (cls == 2 && ka + TT > nk) cls = 1;
     }
     if (cls == 0) continue;
     const lds_d_t* base = smem + (it & 1) * St::kSlot;
-    doublex4 sacc[2], pacc[2];
-    sacc[0] = sacc[1] = splat4(nl);
-    pacc[0] = pacc[1] = splat4(nd);
+    doublex4 sacc[kNT], pacc[kNT];
+#pragma unroll
+    for (int t = 0; t < kNT; ++t) {
+      sacc[t] = splat4(nl);
+      pacc[t] = splat4(nd);
+    }
 #pragma unroll
     for (int s = 0; s < D / 4; ++s)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        sacc[t] = mma(base[St::offA + rimg(4 * s + g, 16 * t + r)], qf[s], sacc[t]);
-        pacc[t] = mma(base[St::offB + rimg(4 * s + g, 16 * t + r)], of[s], pacc[t]);
+      for (int t = 0; t < kNT; ++t) {
+        sacc[t] = mma(base[St::offA + rimg<TT>(4 * s + g, 16 * t + r)], qf[s], sacc[t]);
+        pacc[t] = mma(base[St::offB + rimg<TT>(4 * s + g, 16 * t + r)], of[s], pacc[t]);
       }
-    double ds[2][4];
+    double ds[kNT][4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < kNT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         double pv = exp(sacc[t][i]);
@@ -554,7 +584,7 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
       }
     // dQ[c][q] += Σ_key K[c][key] dSᵀ[key][q]: k-step (t, i) = keys 16t + 4i + g
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < kNT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const lds_d_t* krow = base + St::offAT + (16 * t + 4 * i + g) * St::kP + r;
@@ -589,22 +619,45 @@ hipError_t launch_fwd_t(const FwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int D>
-hipError_t launch_bwd_t(const BwdArgs& a, hipStream_t s) {
+template <int D, int TT = kT, int CH = -1>
+hipError_t launch_dkdv_f64(const BwdArgs& a, hipStream_t s) {
   const int pol = policy_class(a.rule);
-  auto kk = pol == 0 ? bwd_dkdv_f64_kernel<D, 0> : (pol == 1 ? bwd_dkdv_f64_kernel<D, 1> : bwd_dkdv_f64_kernel<D, 2>);
-  auto kq = pol == 0 ? bwd_dq_f64_kernel<D, 0> : (pol == 1 ? bwd_dq_f64_kernel<D, 1> : bwd_dq_f64_kernel<D, 2>);
-  constexpr int smem = bwd64_smem<D>();
+  auto kk = pol == 0 ? bwd_dkdv_f64_kernel<D, 0, TT, CH>
+                     : (pol == 1 ? bwd_dkdv_f64_kernel<D, 1, TT, CH> : bwd_dkdv_f64_kernel<D, 2, TT, CH>);
+  constexpr int smem = bwd64_smem<D, TT>();
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kk), smem);
   if (e != hipSuccess) return e;
-  e = set_smem_once(reinterpret_cast<const void*>(kq), smem);
-  if (e != hipSuccess) return e;
-  const int64_t nkb = (a.rule.k.n + kBM - 1) / kBM, nqb = (a.rule.q.n + kBM - 1) / kBM;
+  const int64_t nkb = (a.rule.k.n + kBM - 1) / kBM;
   hipLaunchKernelGGL(kk, dim3((unsigned)(a.b * nkb)), dim3(kThr), smem, s, a);
-  e = hipGetLastError();
+  return hipGetLastError();
+}
+
+template <int D, int TT = kT>
+hipError_t launch_dq_f64(const BwdArgs& a, hipStream_t s) {
+  const int pol = policy_class(a.rule);
+  auto kq = pol == 0 ? bwd_dq_f64_kernel<D, 0, TT> : (pol == 1 ? bwd_dq_f64_kernel<D, 1, TT> : bwd_dq_f64_kernel<D, 2, TT>);
+  constexpr int smem = bwd64_smem<D, TT>();
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kq), smem);
   if (e != hipSuccess) return e;
+  const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
   hipLaunchKernelGGL(kq, dim3((unsigned)(a.b * nqb)), dim3(kThr), smem, s, a);
   return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_bwd_t(const BwdArgs& a, hipStream_t s) {
+  hipError_t e;
+  if constexpr (D <= 64) {
+    e = launch_dkdv_f64<D>(a, s);
+    if (e != hipSuccess) return e;
+    return launch_dq_f64<D>(a, s);
+  } else {  // 16-column tiles; dK / dV in two channel halves
+    e = launch_dkdv_f64<D, 16, 0>(a, s);
+    if (e != hipSuccess) return e;
+    e = launch_dkdv_f64<D, 16, 1>(a, s);
+    if (e != hipSuccess) return e;
+    return launch_dq_f64<D, 16>(a, s);
+  }
 }
 
 }  // namespace
@@ -621,9 +674,10 @@ hipError_t launch_fwd_f64(const FwdArgs& a, hipStream_t s) {
 }
 
 // backward keeps K·scale, V (dkdv) or Q·scale, dO (dq) plus the dK/dV (dQ) accumulators in
-// registers: 2·D/4 + 2·D/16·4 doubles per lane, which fits up to D = 64
+// registers: 2·D/4 + 2·D/16·4 doubles per lane up to D = 64; at D = 128 the dK/dV pass holds one
+// channel half per launch (2·32 + 2·16 doubles)
 bool bwd_f64_supported(const BwdArgs& a) {
-  return a.d >= 1 && a.v_d >= 1 && a.d <= 64 && a.v_d <= 64 && a.b * ((a.rule.k.n + kBM - 1) / kBM) < (1ll << 31) &&
+  return a.d >= 1 && a.v_d >= 1 && a.d <= 128 && a.v_d <= 128 && a.b * ((a.rule.k.n + kBM - 1) / kBM) < (1ll << 31) &&
          a.b * ((a.rule.q.n + kBM - 1) / kBM) < (1ll << 31);
 }
 
@@ -633,8 +687,10 @@ hipError_t launch_bwd_f64(const BwdArgs& a, hipStream_t s) {
                      a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (max(a.d, a.v_d) <= 32) return launch_bwd_t<32>(a, s);
-  return launch_bwd_t<64>(a, s);
+  const int dm = max(a.d, a.v_d);
+  if (dm <= 32) return launch_bwd_t<32>(a, s);
+  if (dm <= 64) return launch_bwd_t<64>(a, s);
+  return launch_bwd_t<128>(a, s);
 }
 
 }  // namespace fa

@@ -570,8 +570,9 @@ int g_cus = 0;
 int64_t band_workgroups(int64_t n_items) {
   if (g_cus == 0) {
     int dev = 0, cus = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
     g_cus = cus;
   }
   return n_items < g_cus ? n_items : g_cus;
