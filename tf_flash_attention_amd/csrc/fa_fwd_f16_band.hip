@@ -71,6 +71,7 @@ struct BandArgs {
   int64_t n_items;  // b * ceil(nq / kBM)
   int32_t T;        // tile positions per item
   int32_t n_wg;     // workgroups (persistent)
+  int32_t inter;    // 1: XCD-interleaved item order (below)
 };
 
 template <int B, int E, typename F>
@@ -102,10 +103,28 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   const int nq = a.rule.q.n, nk = a.rule.k.n;
   static_assert(T % 4 == 0 && T >= kMinT, "T: a multiple of 4, at least kMinT");
   const int nqb = (nq + kBM - 1) / kBM;
-  // this workgroup's items [it_begin, it_end): contiguous, in (slice, block) order
+  // this workgroup's items: first + stride * local, inside [it_begin, it_end).
+  //   contiguous: a run of consecutive items per workgroup (stride 1);
+  //   XCD-interleaved (inter): the eight XCDs (workgroup g runs on XCD g mod 8) each take one eighth
+  //   of the items, and the J workgroups of an XCD take every J-th item of it, so at any time an
+  //   XCD's CUs walk J consecutive items whose key bands overlap: each K/V tile is re-read from that
+  //   XCD's L2 instead of re-fetched (a contiguous run re-reads a tile one and two items later, a
+  //   window of ~24 tiles per CU that the 4 MB L2 shared by 32 CUs does not hold)
   const int64_t g = blockIdx.x;
-  const int64_t it_begin = g * ba.n_items / ba.n_wg, it_end = (g + 1) * ba.n_items / ba.n_wg;
-  const int n_local = (int)(it_end - it_begin);
+  int64_t it_begin, it_end, first, stride;
+  if (ba.inter) {
+    const int64_t x = g & 7, J = (ba.n_wg - x + 7) >> 3;
+    it_begin = x * ba.n_items / 8;
+    it_end = (x + 1) * ba.n_items / 8;
+    first = it_begin + (g >> 3);
+    stride = J;
+  } else {
+    it_begin = g * ba.n_items / ba.n_wg;
+    it_end = (g + 1) * ba.n_items / ba.n_wg;
+    first = it_begin;
+    stride = 1;
+  }
+  const int n_local = first < it_end ? (int)((it_end - first + stride - 1) / stride) : 0;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -135,7 +154,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   auto make_item = [&](int local) -> Item {
     Item x;
     const bool live = local < n_local;
-    const int64_t n = it_begin + (live ? local : 0);
+    const int64_t n = live ? first + (int64_t)local * stride : it_begin;
     // (64-bit division lowers to VALU code: readfirstlane keeps the results in SGPRs, else every
     // buffer op that takes them in soffset becomes a waterfall loop)
     x.sl = __builtin_amdgcn_readfirstlane((int)(n / nqb - sl0));
@@ -578,6 +597,9 @@ int64_t band_workgroups(int64_t n_items) {
   return n_items < g_cus ? n_items : g_cus;
 }
 
+// the XCD-interleaved item order needs whole XCD groups and several items per workgroup
+bool band_interleaved(int64_t n_items, int64_t n_wg) { return n_wg % 8 == 0 && n_items >= 2 * n_wg; }
+
 struct TCache {
   Rule r;
   int T;
@@ -621,7 +643,7 @@ bool fwd_f16_band_supported(const FwdArgs& a) {
   if (band_tiles_per_item(a) > 24) return false;
   // one descriptor per tensor spans a workgroup's slices: below 2^31 bytes
   const int64_t nqb = (nq + kBM - 1) / kBM, n_items = a.b * nqb, n_wg = band_workgroups(n_items);
-  const int64_t span = (n_items + n_wg - 1) / n_wg / nqb + 2;
+  const int64_t span = (band_interleaved(n_items, n_wg) ? (n_items + 7) / 8 : (n_items + n_wg - 1) / n_wg) / nqb + 2;
   return span * 2 * (int64_t)dm * (nq > nk ? nq : nk) < (1ll << 31);
 }
 
@@ -639,8 +661,11 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   ba.T = band_tiles_per_item(a);
   ba.n_items = a.b * (int64_t)((a.rule.q.n + kBM - 1) / kBM);
   ba.n_wg = (int)band_workgroups(ba.n_items);
+  ba.inter = band_interleaved(ba.n_items, ba.n_wg) ? 1 : 0;
 #ifdef FA_DIAG
-  if (diag_variant("FA_FWD_VARIANT") == 2401 && ba.T == 12) return launch_band_t<12, true>(ba, s);
+  const int dv = diag_variant("FA_FWD_VARIANT");
+  if (dv == 2401 && ba.T == 12) return launch_band_t<12, true>(ba, s);
+  if (dv == 2402) ba.inter = 0;  // round-2 order: contiguous runs of items
 #endif
   switch (ba.T) {
     case 12: return launch_band_t<12>(ba, s);
