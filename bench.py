@@ -184,7 +184,18 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # gloo's rendezvous prints "[Gloo] Rank r is connected to ..." on the process's stdout, where
+        # the driver reads the one JSON line: keep file descriptor 1 on /dev/null while it connects
+        sys.stdout.flush()
+        saved = os.dup(1)
+        devnull = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(devnull, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(devnull)
+            os.close(saved)
     # one process per GPU; modulo only matters when rehearsing N ranks on fewer GPUs
     ndev = max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local % ndev)

@@ -519,6 +519,20 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   // PF & 2: two barriers per step — phase A: the producer's S / dP MFMAs (the consumer stages and
   // reads its operands), phase B: the producer's softmax beside the consumer's dV / dK MFMAs
   constexpr bool TWO = (PF & 2) != 0;
+  // PF & 4 (diagnostic build): per-wave s_memtime sums of each step's parts (stage + barrier, MFMA
+  // part, softmax / hand-over part) written to the unused dQ workspace
+  constexpr bool STAMP = (PF & 4) != 0;
+  uint64_t stv[3] = {0, 0, 0}, st_prev = 0;
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      uint64_t t;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (k >= 0) stv[k] += t - st_prev;
+      st_prev = t;
+    }
+  };
 
   const int nq = a.rule.q.n, nk = a.rule.k.n;
   const uint32_t nkb = (nk + kBK - 1) / kBK;
@@ -527,7 +541,15 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   const int k0 = (int)(bid % nkb) * kBK;  // earliest (heaviest under causal) key blocks first
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = w >> 2, wl = w & 3;     // group 0 produces, group 1 consumes; wl: the key slice
+  const int grp = w >> 2, wl = w & 3;
+  auto stamp_out = [&]() __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      if (lane < 3) {
+        uint64_t v = lane == 0 ? stv[0] : lane == 1 ? stv[1] : stv[2];
+        reinterpret_cast<uint64_t*>(a.ws_dQ)[((int64_t)bid * 8 + w) * 4 + lane] = v;
+      }
+    }
+  };     // group 0 produces, group 1 consumes; wl: the key slice
   const int h = lane >> 5, r = lane & 31;
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const int sig = ((tp & 1) << 1) | (tp >> 1);  // (see the dK/dV kernel above: σ-permuted transposed reads)
@@ -679,7 +701,9 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
     const int ko = (POL == 2) ? seq_order(a.rule.k, a.rule, min(key, nk - 1)) : 0;
     auto pstep = [&](auto C_, int it) __attribute__((always_inline)) {
       constexpr int c = decltype(C_)::value;
+      stamp(-1);
       stage(C_, it);
+      stamp(0);
       const int qa = qt0 + 32 * it;
       const int cls = it < ntiles ? tcls(qa) : 0;
       const lds_char_t* base = smem + c * S::kSlot;
@@ -719,6 +743,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
         }
         if constexpr ((PF & 1) != 0) __builtin_amdgcn_s_setprio(0);
       }
+      stamp(1);
       if constexpr (TWO) __builtin_amdgcn_s_barrier();  // phase B: this softmax beside the consumer's MFMAs
       if (cls == 0) return;
       // P = exp2(S), dS = P∘dP; register i = query 16(i>>3) + 8h + (i&7) = k-step i>>3 of the consumer
@@ -742,6 +767,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
         *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, s_)) = pf[s_];
         *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, 2 + s_)) = sf[s_];
       }
+      stamp(2);
     };
     for (int it = 0; it < nsteps; it += 4) {
       pstep(IC<0>{}, it);
@@ -749,6 +775,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       pstep(IC<2>{}, it + 2);
       pstep(IC<3>{}, it + 3);
     }
+    stamp_out();
     return;
   }
 
@@ -761,7 +788,9 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
     for (int i = 0; i < 16; ++i) { dk[u][i] = 0.f; dv[u][i] = 0.f; }
   auto cstep = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;
+    stamp(-1);
     stage(C_, it);
+    stamp(0);
     const int qa = qt0 + 32 * (it - 1);
     const int cls = (it >= 1 && it - 1 < ntiles) ? tcls(qa) : 0;
     const lds_char_t* base = smem + ((c + 3) % 4) * S::kSlot;
@@ -782,6 +811,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
 #pragma unroll
       for (int n = 0; n < kAh; ++n) rd(n);
     }
+    stamp(1);
     if constexpr (TWO) __builtin_amdgcn_s_barrier();  // phase B: these MFMAs beside the producer's softmax
     if (cls == 0) return;
 #pragma unroll
@@ -791,6 +821,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa[n % (kAh + 1)], pf[s_], dv[u], 0, 0, 0);
       dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa_[n % (kAh + 1)], sf[s_], dk[u], 0, 0, 0);
     }
+    stamp(2);
   };
   for (int it = 0; it < nsteps; it += 4) {
     cstep(IC<0>{}, it);
@@ -798,6 +829,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
     cstep(IC<2>{}, it + 2);
     cstep(IC<3>{}, it + 3);
   }
+  stamp_out();
 
   // ---- dK = scale·Σ dS·Q, dV: rows c = 32u + (i&3) + 8(i>>2) + 4h, column = this lane's key
   if (!wave_active || key >= nk) return;
@@ -1231,6 +1263,8 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
       case 1401: e = launch_dkdv_pc<128, 1>(a, s); break;
       case 1402: e = launch_dkdv_pc<128, 2>(a, s); break;
       case 1403: e = launch_dkdv_pc<128, 3>(a, s); break;
+      case 1404: e = launch_dkdv_pc<128, 4>(a, s); break;  // stamps into the dQ workspace (tools/pc_stamps.py)
+      case 1406: e = launch_dkdv_pc<128, 6>(a, s); break;
       case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
       case 1200: e = launch_dkdv<128, 4, 1>(a, s); break;  // operand reads not run ahead (before the default)
       case 1264: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
