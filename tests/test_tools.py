@@ -54,3 +54,16 @@ def test_shipped_library_has_no_store_hazard():
     assert sum(d.count("buffer_store") + d.count("global_store") for _, d in objs) > 100
     found = []
     assert sum(H.scan_text(n, d, out=found.append) for n, d in objs) == 0, found
+
+
+def test_setup_py_builds_through_make():
+    """setup.py (the reference's setup.py / pyproject counterpart) drives the same make build."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "setup.py", "--name"], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().splitlines()[-1] == "tf_flash_attention_amd"
+    r = subprocess.run([sys.executable, "setup.py", "--dry-run", "build_ext"], cwd=root, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "BuildHip: make -C" in r.stdout and "tf_flash_attention_amd" in r.stdout
