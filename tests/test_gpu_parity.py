@@ -405,10 +405,11 @@ def test_f16_forward_structures(monkeypatch, variant, policy, seq_dims, mode, qs
              seed=int(variant) + d + ws)
 
 
-@pytest.mark.parametrize("variant", ["2300", "2301", "146"])
+@pytest.mark.parametrize("variant", ["2300", "2301", "2399", "146"])
 @pytest.mark.parametrize("policy,seq_dims,mode,qs,ks,ws,causal,d,vd", VARIANT_CASES)
 def test_f16_forward_structures_d128(monkeypatch, variant, policy, seq_dims, mode, qs, ks, ws, causal, d, vd):
-    """d in (64, 128]: the ping-pong kernel (2300 / 2301, forced for local too) and the 4-wave kernel (146)."""
+    """d in (64, 128]: the ping-pong kernel (2300 no priority flips, 2301 the default, 2399 staging at the
+    MFMA-phase head; forced for local too) and the 4-wave kernel (146)."""
     monkeypatch.setenv("FA_FWD_VARIANT", variant)
     run_case(np.float16, policy, seq_dims, mode, (2, 2), d + 64, vd + 32, qs, ks, ws=ws, ls=0, causal=causal,
              bwd=False, seed=int(variant) + d + ws)

@@ -42,13 +42,37 @@ constexpr int kBM = 32 * kNW;         // queries per workgroup
 constexpr int kNS = 3;                // ring slots for K and for V
 constexpr int kQRow = 2 * kBM;        // bytes per Q row in LDS
 constexpr int kTile = kD * kBN * 2;   // 16 KB
-constexpr int kOffK = kD * kQRow;     // Q image [128][256] first (prologue only)
+// K ring, V ring, then the Q image [128][256] (prologue; then the scaled Q fragments): every
+// fragment read and staging store is a lane-constant VGPR base (the ring's offset folded in) plus
+// an immediate below 64 KB, so no address arithmetic runs in the loop
+constexpr int kOffK = 0;
 constexpr int kOffV = kOffK + kNS * kTile;
-constexpr int kSmem = kOffV + kNS * kTile;  // 160 KB
+constexpr int kOffQ = kOffV + kNS * kTile;
+constexpr int kSmem = kOffQ + kD * kQRow;  // 160 KB
 constexpr int kCPT = kD * 8 / (kNW * 64);   // 16-B chunks per thread per tile (2)
 constexpr float kRescaleThr = 8.f;
 
 constexpr int kFPrio = 1;  // s_setprio 1 over each MFMA phase
+constexpr int kFStamp = 2;  // diagnostic: per-wave s_memtime sums per phase part, written over l (l garbage)
+constexpr int kFPipe = 32;      // MFMA phase software-pipelined: every fragment read follows the MFMA that frees it
+constexpr int kFStAfterQK0 = 64;   // staging stores + loads after Sᵀ half 0 instead of first
+constexpr int kFStAfterPV0 = 128;  // ... after PV half 0
+constexpr int kFEarlyKQ = 256;     // K(i+1) / Q half-0 reads right after Sᵀ half 1 (before PV half 1)
+constexpr int kFStampVm = 16384;  // diagnostic: with kFStamp, stamp the staging loads' wait separately
+constexpr int kFStampSt = 32768;  // ... and the staging stores apart from the loads
+constexpr int kFClsAhead = 524288;  // tile classes of the next MFMA phase computed at the end of the softmax phase
+constexpr int kFSpread = 262144;  // staging store + load of one chunk before each of the four MFMA blocks
+constexpr int kFDefault = kFPrio | kFClsAhead | kFSpread;  // round 2: c3 forward 2.53-2.55 -> 2.43-2.50 ms
+constexpr int kADma = 131072;  // ablation (results wrong: no ordering): staging by LDS-DMA in place of load + store
+constexpr int kFLoadsValu = 65536;  // staging loads issued in the softmax phase (no memory traffic otherwise)
+constexpr int kFStampFine = 8;  // diagnostic: with kFStamp, also stamp the parts of the MFMA phase
+constexpr int kANoSoftmax = 4;  // ablation (results wrong): the VALU phase only converts S to P
+constexpr int kANoStLoad = 512;    // ablation (results wrong): no staging loads (stale registers stored)
+constexpr int kANoStStore = 1024;  // ablation (results wrong): no staging stores
+constexpr int kARotate = 2048;     // ablation (results wrong): staging loads of workgroup b shifted by b mod 16 tiles
+constexpr int kAContig = 8192;     // ablation (results wrong): each staged tile read as one contiguous 16 KB block
+constexpr int kFRot = 4096;        // the key tiles walked from a per-block start (block mod 16), wrapping
+constexpr int kAHotTile = 16;   // ablation (results wrong): every staging load re-reads the first K / V tile
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArgs a) {
@@ -80,6 +104,19 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
   if (POL != 0) k_range_for_q_block(a.rule, q0, qlast, &kb, &ke);
   const int kt0 = (kb / kBN) * kBN;
   const int ntiles = (ke > kb) ? (ke - kt0 + kBN - 1) / kBN : 0;
+  // position it of the key loop -> key offset of its tile.  kFRot: the concurrently running blocks of
+  // a slice start at different tiles; positions past the last tile stay past it (zero tiles)
+  const int rot = ((F & kFRot) != 0 && ntiles > 0) ? (int)((bid % nqb) & 15) % ntiles : 0;
+  auto tk0 = [&](int it) -> int __attribute__((always_inline)) {
+    int t = it;
+    if constexpr ((F & kFRot) != 0) {
+      if (it >= 0 && it < ntiles) {
+        t = it + rot;
+        t = t >= ntiles ? t - ntiles : t;
+      }
+    }
+    return kt0 + t * kBN;
+  };
 
   // ---- staging: chunk j of this thread = 8 keys (16 B) of channel row (tid + 512 j) >> 3
   const int cm = tid & 7;
@@ -91,12 +128,21 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
     koff[j] = c < d ? go : 0x80000000u;
     voff[j] = c < vd ? go : 0x80000000u;
     kwo[j] = c * 128 + ((cm * 16) ^ ((c & 2) << 5));
-    vwo[j] = c * 128 + 16 * (cm ^ ((c >> 1) & 7));
+    vwo[j] = kOffV + c * 128 + 16 * (cm ^ ((c >> 1) & 7));  // the V ring's offset folded in
+    asm volatile("" : "+v"(vwo[j]));
   }
   // branch-free (exact vmcnt waits): chunks past nk — the tail, tiles past the end — read as zeros
   auto load = [&](u32x4 (&dst)[kCPT], __amdgpu_buffer_rsrc_t rs, const uint32_t (&off)[kCPT], int k0)
       __attribute__((always_inline)) {
     const bool in = k0 + 8 * cm < nk;
+    if constexpr ((F & kAContig) != 0) {
+#pragma unroll
+      for (int j = 0; j < kCPT; ++j) {
+        const uint32_t co = (uint32_t)((tid + kNW * 64 * j) >> 3) * 128u + 16u * cm;
+        dst[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, in ? co : 0x80000000u, 256 * min(k0, nk - kBN), 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < kCPT; ++j)
       dst[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off[j] : 0x80000000u, 2 * min(k0, nk), 0);
@@ -110,9 +156,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
   u32x4 kst[kCPT], vst[kCPT];
   {
     u32x4 k0v[kCPT], k1v[kCPT], v0v[kCPT];
-    load(k0v, krs, koff, kt0);
-    load(k1v, krs, koff, kt0 + kBN);
-    load(v0v, vrs, voff, kt0);
+    load(k0v, krs, koff, tk0(0));
+    load(k1v, krs, koff, tk0(1));
+    load(v0v, vrs, voff, tk0(0));
     // Q [128][256], 64-B blocks XOR-swizzled by c&3: all of a thread's loads before its stores
     constexpr int kQPT = kD * (kBM / 8) / (kNW * 64);
     u32x4 qv[kQPT];
@@ -124,13 +170,13 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
 #pragma unroll
     for (int j = 0; j < kQPT; ++j) {
       const int idx = tid + j * kNW * 64, c = idx / (kBM / 8), m = idx % (kBM / 8);
-      *reinterpret_cast<lds_u32x4_t*>(smem + c * kQRow + ((m * 16) ^ ((c & 3) << 6))) = qv[j];
+      *reinterpret_cast<lds_u32x4_t*>(smem + kOffQ + c * kQRow + ((m * 16) ^ ((c & 3) << 6))) = qv[j];
     }
     store(kOffK, kwo, k0v);
     store(kOffK + kTile, kwo, k1v);
-    store(kOffV, vwo, v0v);
-    load(kst, krs, koff, kt0 + 2 * kBN);
-    load(vst, vrs, voff, kt0 + kBN);
+    store(0, vwo, v0v);
+    load(kst, krs, koff, tk0(2));
+    load(vst, vrs, voff, tk0(1));
   }
   __syncthreads();
 
@@ -146,7 +192,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
       for (int e = 0; e < 2; ++e) {
         const int cr = 16 * s + 8 * (g >> 1) + 4 * e + tq;
         const int col = 32 * w + 16 * (g & 1) + 4 * tp;
-        const half4 t = tr_read(smem + cr * kQRow + ((col * 2) ^ ((cr & 3) << 6)));
+        const half4 t = tr_read(smem + kOffQ + cr * kQRow + ((col * 2) ^ ((cr & 3) << 6)));
         if (e == 0) qf[s].lo = t; else qf[s].hi = t;
       }
       qf[s] = scale8(qf[s], c2);
@@ -154,9 +200,10 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
     __syncthreads();  // every wave has its fragments before the image is overwritten
 #pragma unroll
     for (int s = 0; s < kD / 16; ++s)
-      *reinterpret_cast<lds_half8_t*>(smem + 8192 * w + 1024 * s + 16 * lane) = qf[s];
+      *reinterpret_cast<lds_half8_t*>(smem + kOffQ + 8192 * w + 1024 * s + 16 * lane) = qf[s];
   }
-  const uint32_t qfrag = 8192 * w + 16 * lane;
+  uint32_t qfrag = kOffQ + 8192 * w + 16 * lane;
+  asm volatile("" : "+v"(qfrag));  // opaque: the 96 KB stays in the VGPR, the k-step offset in the immediate
   half8 qh[4];  // Q fragments of one channel half
   auto read_q = [&](int half) __attribute__((always_inline)) {
 #pragma unroll
@@ -180,7 +227,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
   // tile class for this wave: 0 no allowed pair (skipped), 1 mixed (masked), 2 all allowed
   auto tcls = [&](int it) -> int __attribute__((always_inline)) {
     if (it < 0 || it >= ntiles) return 0;
-    const int k0 = kt0 + it * kBN, k1 = k0 + kBN - 1;
+    const int k0 = tk0(it), k1 = k0 + kBN - 1;
     if (POL == 0) return (k1 < nk) ? 2 : 1;
     if (!wave_active || wlo_min > k1 || whi_max < k0) return 0;
     return (wlo_max <= k0 && whi_min >= k1 && k1 < nk) ? 2 : 1;
@@ -195,7 +242,10 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
     kbase[t] = (8 * (g >> 1) + tq) * 128 + (((32 * t + 16 * (g & 1) + 4 * sig) * 2) ^ ((tq & 2) << 5));
   uint32_t vbase[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) vbase[s] = r * 128 + 16 * ((2 * s + h) ^ ((r >> 1) & 7));
+  for (int s = 0; s < 4; ++s) {
+    vbase[s] = kOffV + r * 128 + 16 * ((2 * s + h) ^ ((r >> 1) & 7));
+    asm volatile("" : "+v"(vbase[s]));  // the V ring's offset stays in the VGPR (see kOffQ)
+  }
 
   half8 kf[2][4];  // K fragments of one channel half: k-steps 4·half + 0..3
   half8 vf[4][2];  // V fragments of one row half: rows 64·half + 32u + r
@@ -211,7 +261,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
       }
   };
   auto read_v = [&](int slot, int half) __attribute__((always_inline)) {
-    const lds_char_t* p = smem + kOffV + slot * kTile;
+    const lds_char_t* p = smem + slot * kTile;  // kOffV is in vbase
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -257,7 +307,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
       st[0][i] -= m_run;
       st[1][i] -= m_run;
     }
-    if (cls == 1) mask(kt0 + it * kBN);
+    if (cls == 1) mask(tk0(it));
     float mx[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) mx[j] = fmaxf(st[j >> 1][8 * (j & 1)], st[j >> 1][8 * (j & 1) + 1]);
@@ -317,45 +367,257 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
         o[2 * half + u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[2 * half + u], 0, 0, 0);
     }
   };
+  uint64_t st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if constexpr ((F & kFStamp) != 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      uint64_t t;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (k >= 0) st_acc[k] += t - st_prev;
+      st_prev = t;
+    }
+  };
+
+  auto fine = [&](int k) __attribute__((always_inline)) {
+    if constexpr ((F & kFStampFine) != 0) stamp(k);
+  };
+  // kFClsAhead: the scalar tile-class work of MFMA(it+1) runs at the end of VALU(it), where the SALU
+  // is idle, instead of at the head of the MFMA phase (wave-uniform: kept in SGPRs over the barrier)
+  int cls_q = tcls(0), cls_p = 0;  // classes of the tiles of the next Sᵀ (it) and PV (it - 1)
   auto mfma_phase = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;  // it mod 3
+    constexpr int kSt = (F & (kFStampVm | kFSpread)) ? 3 : (F & kFStAfterQK0) ? 1 : (F & kFStAfterPV0) ? 2 : 0;
+    // kFSpread: chunk q (K0, K1, V0, V1) stored and re-loaded before MFMA block q, so each
+    // group's 16 loads and 16 stores reach the TA / LDS a quarter at a time under the MFMAs
+    auto stage1 = [&](int q) __attribute__((always_inline)) {
+      if constexpr ((F & kFSpread) != 0) {
+        const int j = q & 1;
+        if (q < 2) {
+          *reinterpret_cast<lds_u32x4_t*>(smem + kOffK + ((c + 2) % kNS) * kTile + kwo[j]) = kst[j];
+          const int k0 = tk0(it + 3);
+          kst[j] = __builtin_amdgcn_raw_buffer_load_b128(krs, (k0 + 8 * cm < nk) ? koff[j] : 0x80000000u, 2 * min(k0, nk), 0);
+        } else {
+          *reinterpret_cast<lds_u32x4_t*>(smem + ((c + 1) % kNS) * kTile + vwo[j]) = vst[j];
+          const int k0 = tk0(it + 2);
+          vst[j] = __builtin_amdgcn_raw_buffer_load_b128(vrs, (k0 + 8 * cm < nk) ? voff[j] : 0x80000000u, 2 * min(k0, nk), 0);
+        }
+      }
+    };
     if (F & kFPrio) __builtin_amdgcn_s_setprio(1);
     // (unconditional: past the end these move zeros into slots nobody reads unmasked)
-    store(kOffK + ((c + 2) % kNS) * kTile, kwo, kst);  // K(i+2) over K(i-1)
-    store(kOffV + ((c + 1) % kNS) * kTile, vwo, vst);  // V(i+1) over V(i-2)
-    load(kst, krs, koff, kt0 + (it + 3) * kBN);
-    load(vst, vrs, voff, kt0 + (it + 2) * kBN);
-    const bool dq = tcls(it) != 0, dp = tcls(it - 1) != 0;
+    auto staging = [&]() __attribute__((always_inline)) {
+      if constexpr ((F & kADma) != 0) {
+#pragma unroll
+        for (int j = 0; j < kCPT; ++j) {
+          const int k0 = tk0(it + 3);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (__attribute__((address_space(3))) void*)(smem + ((c + 2) % kNS) * kTile + 1024 * (w + 8 * j)), 16,
+                                                   (k0 + 8 * cm < nk) ? koff[j] : 0x80000000u, 2 * min(k0, nk), 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < kCPT; ++j) {
+          const int k0 = tk0(it + 2);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (__attribute__((address_space(3))) void*)(smem + kOffV + ((c + 1) % kNS) * kTile + 1024 * (w + 8 * j)), 16,
+                                                   (k0 + 8 * cm < nk) ? voff[j] : 0x80000000u, 2 * min(k0, nk), 0, 0);
+        }
+        return;
+      }
+      if constexpr ((F & kANoStStore) == 0) {
+        store(kOffK + ((c + 2) % kNS) * kTile, kwo, kst);  // K(i+2) over K(i-1)
+        store(((c + 1) % kNS) * kTile, vwo, vst);  // V(i+1) over V(i-2)
+      }
+      if constexpr ((F & kFStampSt) != 0) stamp(8);
+      if constexpr ((F & (kANoStLoad | kFLoadsValu)) == 0) {
+        const int arot = (F & kARotate) ? (int)(bid % 16) : 0;
+        if constexpr ((F & (kAHotTile | kARotate)) != 0) {
+          load(kst, krs, koff, kt0 + ((F & kAHotTile) ? 0 : ((it + 3 + arot) % max(ntiles, 1)) * kBN));
+          load(vst, vrs, voff, kt0 + ((F & kAHotTile) ? 0 : ((it + 2 + arot) % max(ntiles, 1)) * kBN));
+        } else {
+          load(kst, krs, koff, tk0(it + 3));
+          load(vst, vrs, voff, tk0(it + 2));
+        }
+      }
+    };
+    if constexpr ((F & kFStampVm) != 0) {
+      stamp(5);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp(6);
+      staging();
+      stamp(7);
+    } else if constexpr (kSt == 0) {
+      staging();
+    }
+    const bool dq = ((F & kFClsAhead) ? cls_q : tcls(it)) != 0, dp = ((F & kFClsAhead) ? cls_p : tcls(it - 1)) != 0;
+    fine(5);
+    stage1(0);
     if (dq) qk(0);
+    if constexpr (kSt == 1) staging();
+    fine(6);
+    stage1(1);
     read_k(c, 1);
     read_q(1);
     if (dp) pv(0);
+    if constexpr (kSt == 2) staging();
+    fine(7);
+    stage1(2);
     read_v((c + 2) % kNS, 1);
     if (dq) qk(1);
+    fine(8);
+    stage1(3);
+    if constexpr ((F & kFEarlyKQ) != 0) {
+      read_k((c + 1) % kNS, 0);
+      read_q(0);
+    }
     if (dp) pv(1);
+    fine(9);
     // this phase's stores are complete before its barrier: the other group reads K(i+2) / V(i+1)
     // at the end of the next interval (the reads above were already waited for by the MFMAs)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    read_k((c + 1) % kNS, 0);
-    read_q(0);
+    if constexpr ((F & kFEarlyKQ) == 0) {
+      read_k((c + 1) % kNS, 0);
+      read_q(0);
+    }
     read_v(c, 0);
     if (F & kFPrio) __builtin_amdgcn_s_setprio(0);
   };
+  // The pipelined MFMA phase (kFPipe): the 32 MFMAs run unconditionally (P is zero for a skipped
+  // tile, S of a skipped tile is never read) so the phase is one basic block, and each fragment
+  // read is pinned right after the MFMA pair that frees its registers (sched_group_barrier):
+  //   Sᵀ half 0, pair s:  then K(i) half-1 reads of k-step 4+s, Q half-1 read s
+  //   PV half 0, pair s:  then V(i-1) rows 64.. reads of s
+  //   Sᵀ half 1, pair s:  then K(i+1) half-0 reads of k-step s, Q half-0 read s
+  //   PV half 1, pair s:  then V(i) rows 0.. reads of s, and one staging store + its next load
+  // so the LDS traffic (2.5 reads per MFMA at most) issues under the matrix pipe instead of
+  // between MFMA blocks.
+  auto mfma_phase_pipe = [&](auto C_, int it) __attribute__((always_inline)) {
+    constexpr int c = decltype(C_)::value;  // it mod 3
+    if (F & kFPrio) __builtin_amdgcn_s_setprio(1);
+    const lds_char_t* pkc = smem + kOffK + c * kTile;              // K(i)
+    const lds_char_t* pkn = smem + kOffK + ((c + 1) % kNS) * kTile;  // K(i+1)
+    const lds_char_t* pvp = smem + ((c + 2) % kNS) * kTile;  // V(i-1) (kOffV is in vbase)
+    const lds_char_t* pvc = smem + c * kTile;              // V(i)
+    const floatx16 zero = {};
+    // one MFMA pair and the reads it frees registers for per scheduling region
+    auto gap = [&](auto NR_, auto ST_) __attribute__((always_inline)) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, decltype(NR_)::value, 0);
+      if constexpr (decltype(ST_)::value != 0) {
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], qh[s], s == 0 ? zero : st[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        kf[t][s].lo = tr_read(pkc + kbase[t] + (16 * (4 + s)) * 128);
+        kf[t][s].hi = tr_read(pkc + kbase[t] + (16 * (4 + s) + 4) * 128);
+      }
+      qh[s] = read_b128(smem + qfrag + 1024 * (4 + s));
+      gap(IC<5>{}, IC<0>{});
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const half8 p = __builtin_bit_cast(half8, u32x4{pw[s][0], pw[s][1], pw[s][2], pw[s][3]});
+#pragma unroll
+      for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[u], 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) vf[s][u] = read_b128(pvp + vbase[s] + (64 + 32 * u) * 128);
+      gap(IC<2>{}, IC<0>{});
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], qh[s], st[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        kf[t][s].lo = tr_read(pkn + kbase[t] + (16 * s) * 128);
+        kf[t][s].hi = tr_read(pkn + kbase[t] + (16 * s + 4) * 128);
+      }
+      qh[s] = read_b128(smem + qfrag + 1024 * s);
+      gap(IC<5>{}, IC<0>{});
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const half8 p = __builtin_bit_cast(half8, u32x4{pw[s][0], pw[s][1], pw[s][2], pw[s][3]});
+#pragma unroll
+      for (int u = 0; u < 2; ++u) o[2 + u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[2 + u], 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) vf[s][u] = read_b128(pvc + vbase[s] + (32 * u) * 128);
+      // staging: K(i+2) over K(i-1), V(i+1) over V(i-2); then the next loads into the freed registers
+      // (unconditional: past the end these move zeros into slots nobody reads unmasked)
+      if (s < 2) {
+        *reinterpret_cast<lds_u32x4_t*>(smem + kOffK + ((c + 2) % kNS) * kTile + kwo[s]) = kst[s];
+        const int k0 = tk0(it + 3);
+        kst[s] = __builtin_amdgcn_raw_buffer_load_b128(krs, (k0 + 8 * cm < nk) ? koff[s] : 0x80000000u, 2 * min(k0, nk), 0);
+      } else {
+        *reinterpret_cast<lds_u32x4_t*>(smem + ((c + 1) % kNS) * kTile + vwo[s - 2]) = vst[s - 2];
+        const int k0 = tk0(it + 2);
+        vst[s - 2] = __builtin_amdgcn_raw_buffer_load_b128(vrs, (k0 + 8 * cm < nk) ? voff[s - 2] : 0x80000000u, 2 * min(k0, nk), 0);
+      }
+      gap(IC<2>{}, IC<1>{});
+    }
+    // this phase's stores are complete before its barrier (the other group reads these tiles from
+    // its next MFMA phase on): all but the six reads issued after the last store
+    __builtin_amdgcn_s_waitcnt(0xC67F);  // lgkmcnt(6)
+    if (F & kFPrio) __builtin_amdgcn_s_setprio(0);
+  };
   auto valu_phase = [&](int it) __attribute__((always_inline)) {
-    const int cls = tcls(it);
-    if (cls != 0) softmax(it, cls);
+    if constexpr ((F & kFLoadsValu) != 0) {  // the tiles this group stores at the start of MFMA(it+1)
+      load(kst, krs, koff, tk0(it + 3));
+      load(vst, vrs, voff, tk0(it + 2));
+    }
+    const int cls = (F & kFClsAhead) ? cls_q : tcls(it);
+    if constexpr ((F & kFPipe) != 0) {
+      if (cls == 0) {  // the next (unconditional) PV must add nothing
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y) pw[x][y] = 0u;
+      }
+    }
+    if constexpr ((F & kANoSoftmax) != 0) {
+      if (cls != 0) exp_cvt();
+    } else {
+      if (cls != 0) softmax(it, cls);
+    }
+    if constexpr ((F & kFClsAhead) != 0) {
+      cls_p = cls;
+      cls_q = tcls(it + 1);
+    }
   };
 
   // both groups run the same loop; group 1 enters it one barrier late (see fa_fwd_f16_pingpong.hip)
   read_k(0, 0);
   read_q(0);
+  if constexpr ((F & kFPipe) != 0) {
+    read_v(0, 0);  // the first (unconditional) PV multiplies these by P = 0
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) pw[x][y] = 0u;
+  }
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   if (grp == 1) __builtin_amdgcn_s_barrier();
   auto iter = [&](auto C_, int it) __attribute__((always_inline)) {
+    stamp(-1);
     __builtin_amdgcn_s_barrier();
-    mfma_phase(C_, it);
+    stamp(0);
+    if constexpr ((F & kFPipe) != 0)
+      mfma_phase_pipe(C_, it);
+    else
+      mfma_phase(C_, it);
+    stamp(1);
     __builtin_amdgcn_s_barrier();
+    stamp(2);
     valu_phase(it);
+    stamp(3);
+    if constexpr ((F & kFStamp) != 0) st_acc[4] += 1;
   };
   for (int it = 0; it <= ntiles; it += kNS) {
     iter(IC<0>{}, it);
@@ -389,6 +651,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
       mo[qi] = neg_inf_approx<__half>();
     }
   }
+  if constexpr ((F & kFStamp) != 0) {  // diagnostic build: stamps over this wave's first l entries
+    if (lane < 10 && wq0 + lane < nq) {
+      uint64_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 10; ++k) v = (lane == k) ? st_acc[k] : v;
+      static_cast<float*>(a.l)[bi * (int64_t)nq + wq0 + lane] = (float)v;
+    }
+  }
 }
 
 template <int F>
@@ -414,9 +684,56 @@ bool fwd_f16_pingpong128_supported(const FwdArgs& a) {
 
 hipError_t launch_fwd_f16_pingpong128(const FwdArgs& a, hipStream_t s) {
 #ifdef FA_DIAG
-  if (diag_variant("FA_FWD_VARIANT") == 2300) return launch_t<0>(a, s);
+  switch (diag_variant("FA_FWD_VARIANT")) {
+    case 2300: return launch_t<0>(a, s);
+    case 2399: return launch_t<kFPrio>(a, s);  // the round-2 baseline (staging at the phase head)
+    case 2301: return launch_t<kFDefault>(a, s);  // the default, forced for every rule (tests)
+    case 2361: return launch_t<kFPrio | kFStamp>(a, s);
+    case 2302: return launch_t<kFPrio | kFStamp | kANoSoftmax>(a, s);
+    case 2303: return launch_t<kFPrio | kANoSoftmax>(a, s);
+    case 2304: return launch_t<kFPrio | kFStamp | kFStampFine>(a, s);
+    case 2305: return launch_t<kFPrio | kFStamp | kFStampFine | kANoSoftmax>(a, s);
+    case 2306: return launch_t<kFPrio | kFStamp | kFStampFine | kAHotTile>(a, s);
+    case 2307: return launch_t<kFPrio | kAHotTile>(a, s);
+    case 2320: return launch_t<kFPrio | kFStAfterQK0>(a, s);
+    case 2321: return launch_t<kFPrio | kFStAfterPV0>(a, s);
+    case 2322: return launch_t<kFPrio | kFEarlyKQ>(a, s);
+    case 2323: return launch_t<kFPrio | kFStAfterQK0 | kFEarlyKQ>(a, s);
+    case 2324: return launch_t<kFPrio | kFStAfterPV0 | kFEarlyKQ>(a, s);
+    case 2325: return launch_t<kFPrio | kFStAfterQK0 | kFStamp | kFStampFine>(a, s);
+    case 2326: return launch_t<kFPrio | kANoStLoad>(a, s);
+    case 2327: return launch_t<kFPrio | kANoStStore>(a, s);
+    case 2328: return launch_t<kFPrio | kANoStLoad | kANoStStore>(a, s);
+    case 2329: return launch_t<kFPrio | kANoStLoad | kFStamp | kFStampFine>(a, s);
+    case 2330: return launch_t<kFPrio | kANoStStore | kFStamp | kFStampFine>(a, s);
+    case 2331: return launch_t<kFPrio | kARotate>(a, s);
+    case 2332: return launch_t<kFPrio | kARotate | kFStamp | kFStampFine>(a, s);
+    case 2340: return launch_t<kFPrio | kFRot>(a, s);
+    case 2341: return launch_t<kFPrio | kFRot | kFStamp | kFStampFine>(a, s);
+    case 2342: return launch_t<kFPrio | kFRot | kFStAfterQK0>(a, s);
+    case 2343: return launch_t<kFPrio | kAContig>(a, s);
+    case 2344: return launch_t<kFPrio | kAContig | kFStamp | kFStampFine>(a, s);
+    case 2345: return launch_t<kFPrio | kFStamp | kFStampVm>(a, s);
+    case 2346: return launch_t<kFPrio | kFStamp | kFStampVm | kAHotTile>(a, s);
+    case 2347: return launch_t<kFPrio | kFStamp | kFStampVm | kFStampSt>(a, s);
+    case 2350: return launch_t<kFPrio | kFLoadsValu>(a, s);
+    case 2351: return launch_t<kFPrio | kFLoadsValu | kFStamp | kFStampFine>(a, s);
+    case 2352: return launch_t<kFPrio | kFLoadsValu | kFStAfterQK0>(a, s);
+    case 2353: return launch_t<kFPrio | kADma>(a, s);
+    case 2354: return launch_t<kFPrio | kADma | kFStamp | kFStampFine>(a, s);
+    case 2355: return launch_t<kFPrio | kFSpread>(a, s);
+    case 2356: return launch_t<kFPrio | kFSpread | kFStamp | kFStampFine>(a, s);
+    case 2357: return launch_t<kFPrio | kFSpread | kFRot>(a, s);
+    case 2358: return launch_t<kFPrio | kFClsAhead>(a, s);
+    case 2359: return launch_t<kFPrio | kFClsAhead | kFStamp | kFStampFine>(a, s);
+    case 2360: return launch_t<kFPrio | kFClsAhead | kFSpread>(a, s);
+    case 2310: return launch_t<kFPrio | kFPipe>(a, s);
+    case 2311: return launch_t<kFPrio | kFPipe | kFStamp>(a, s);
+    case 2312: return launch_t<kFPipe>(a, s);
+    default: break;
+  }
 #endif
-  return launch_t<kFPrio>(a, s);
+  return launch_t<kFDefault>(a, s);
 }
 
 }  // namespace fa
