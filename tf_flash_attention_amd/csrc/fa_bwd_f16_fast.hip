@@ -872,7 +872,7 @@ struct DqSmem {
 };
 
 // dQ: query-outer.  One workgroup = NW waves x 32 queries of one (batch, head) slice.
-template <int D, int NW, int WPE, int POL, bool ALN, bool PRE = false>
+template <int D, int NW, int WPE, int POL, bool ALN, bool PRE = false, int SPR = 0>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -1021,6 +1021,19 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
       *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[set][j];
     }
   };
+  // SPR: one chunk's store and re-load at a time, between the Sᵀ / dPᵀ MFMA pairs (one wave per SIMD:
+  // a 1 KB load or a 16-B-per-lane store issued at the step head holds the wave for tens of cycles
+  // each while the matrix pipe idles)
+  auto stage_chunk = [&](int slot, int set, int j, int ka) __attribute__((always_inline)) {
+    const bool isV = is_v(j);
+    if constexpr (SPR == 1)
+      *reinterpret_cast<lds_u32x4_t*>(smem + slot * S::kSlot + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[set][j];
+    const bool out = ka + 8 * cm >= nk;
+    if constexpr (ALN)
+      kr[set][j] = buf_load16(isV ? vrs : krs, voff[j], 2 * min(ka, nk), out || crow_[j] >= (isV ? vd : d));
+    else
+      kr[set][j] = buf_load8h(isV ? vrs : krs, voff[j], ka + 8 * cm, nk, crow_[j] < (isV ? vd : d));
+  };
 
   floatx16 dq[D / 32];
 #pragma unroll
@@ -1052,10 +1065,13 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     constexpr int p = decltype(P_)::value;
     __syncthreads();
     const int ka = kt0 + it * kBN;
-    // unconditional (past the end they move zeros into a slot nobody reads): exact vmcnt waits
-    store_tile(p ^ 1, p ^ 1);
-    load_tile(ka + 3 * kBN, p ^ 1);
     const int cls = it < ntiles ? tcls(ka) : 0;  // (the loop's last pair may end on a phantom step)
+    // unconditional (past the end they move zeros into a slot nobody reads): exact vmcnt waits
+    if (SPR == 2 || (SPR != 0 && cls == 0)) store_tile(p ^ 1, p ^ 1);  // (SPR 2: the loads alone spread)
+    if (SPR == 0 || cls == 0) {
+      if (SPR == 0) store_tile(p ^ 1, p ^ 1);
+      load_tile(ka + 3 * kBN, p ^ 1);
+    }
     if (cls == 0) return;
     const lds_char_t* base = smem + p * S::kSlot;
     floatx16 st[2], dp[2];
@@ -1078,8 +1094,12 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
       };
       rd(0);
       rd(1);
+      static_assert(!SPR || kN % kCPT == 0, "staging chunks spread over the MFMA pairs");
 #pragma unroll
       for (int n = 0; n < kN; ++n) {
+        if constexpr (SPR) {
+          if (n % (kN / kCPT) == 0) stage_chunk(p ^ 1, p ^ 1, n / (kN / kCPT), ka + 3 * kBN);
+        }
         if (n + 2 < kN) rd(n + 2);
         if (n == kN - 2) rka(0);
         if (n == kN - 1) rka(1);
@@ -1205,17 +1225,17 @@ hipError_t launch_dkdv_pc(const BwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int D, int NW, int WPE, bool PRE = false>
+template <int D, int NW, int WPE, bool PRE = false, int SPR = 0>
 hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
   using S = DqSmem<D, NW>;
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
   const int pol = bwd_pol(a.rule);
-  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, true, PRE>
-                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, true, PRE>
-                                                      : bwd_dq_kernel<D, NW, WPE, 2, true, PRE>)
-                                        : (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, false, PRE>
-                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, false, PRE>
-                                                      : bwd_dq_kernel<D, NW, WPE, 2, false, PRE>);
+  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, true, PRE, SPR>
+                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, true, PRE, SPR>
+                                                      : bwd_dq_kernel<D, NW, WPE, 2, true, PRE, SPR>)
+                                        : (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, false, PRE, SPR>
+                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, false, PRE, SPR>
+                                                      : bwd_dq_kernel<D, NW, WPE, 2, false, PRE, SPR>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(NW * 64), S::kTotal, s, a);
@@ -1281,6 +1301,8 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
     }
     if (e != hipSuccess) return e;
     if (v == 1200 || v == 1264) return launch_dq<128, 4, 1>(a, s);
+    if (v == 1500) return launch_dq<128, 4, 1, true, 1>(a, s);  // staging spread over the MFMA pairs
+    if (v == 1501) return launch_dq<128, 4, 1, true, 2>(a, s);  // ... the loads only
     return launch_dq<128, 4, 1, true>(a, s);
   }
 #endif
