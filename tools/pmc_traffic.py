@@ -20,9 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def counter_means(root, regex):
-    """Per counter: the sum over matching kernels of each kernel's mean per dispatch (a step that
-    launches several kernels, e.g. forward + backward, is priced as one step), and the dispatches."""
+def counter_values(root, regex):
     vals = {}
     for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True)):
         with open(f) as fh:
@@ -30,8 +28,24 @@ def counter_means(root, regex):
                 name = row.get("Kernel_Name", "")
                 if regex.search(name):
                     vals.setdefault(row["Counter_Name"], {}).setdefault(name, []).append(float(row["Counter_Value"]))
+    return vals
+
+
+def counter_means(root, regex):
+    """Per counter: the sum over matching kernels of each kernel's mean per dispatch (a step that
+    launches several kernels, e.g. forward + backward, is priced as one step), and the dispatches."""
     return {c: (sum(sum(v) / len(v) for v in per.values()), sum(len(v) for v in per.values()))
-            for c, per in vals.items()}
+            for c, per in counter_values(root, regex).items()}
+
+
+def per_kernel(root, regex):
+    """Corrected read / write bytes per launch of each matching kernel (where a step's traffic goes)."""
+    vals = counter_values(root, regex)
+    out = {}
+    for c, scale, key in (("FETCH_SIZE", 2048, "read_bytes"), ("WRITE_SIZE", 1024, "write_bytes")):
+        for name, v in vals.get(c, {}).items():
+            out.setdefault(name, {})[key] = sum(v) / len(v) * scale
+    return out
 
 
 def algorithmic_bytes(cfg_key):
@@ -64,6 +78,7 @@ def main():
         "algorithmic_read_bytes": alg_r, "algorithmic_write_bytes": alg_w,
         "traffic_over_algorithmic": (read_b + write_b) / (alg_r + alg_w),
         "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read half-count); WRITE_SIZE KiB x1024",
+        "per_kernel": per_kernel(a.root, re.compile(a.regex)),
     }
     path = a.out or os.path.join(ROOT, "profiles", f"traffic_{a.cfg}.json")
     os.makedirs(os.path.dirname(path), exist_ok=True)
