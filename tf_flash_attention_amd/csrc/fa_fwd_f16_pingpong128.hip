@@ -60,9 +60,11 @@ constexpr int kFStAfterPV0 = 128;  // ... after PV half 0
 constexpr int kFEarlyKQ = 256;     // K(i+1) / Q half-0 reads right after Sᵀ half 1 (before PV half 1)
 constexpr int kFStampVm = 16384;  // diagnostic: with kFStamp, stamp the staging loads' wait separately
 constexpr int kFStampSt = 32768;  // ... and the staging stores apart from the loads
+constexpr int kFReadsValu = 1048576;  // the next MFMA phase's first fragments read at the head of the softmax phase
 constexpr int kFClsAhead = 524288;  // tile classes of the next MFMA phase computed at the end of the softmax phase
 constexpr int kFSpread = 262144;  // staging store + load of one chunk before each of the four MFMA blocks
-constexpr int kFDefault = kFPrio | kFClsAhead | kFSpread;  // round 2: c3 forward 2.53-2.55 -> 2.43-2.50 ms
+constexpr int kFPkSub = 2097152;  // the running-reference subtraction as packed fp32 (v_pk_add_f32, two scores each)
+constexpr int kFDefault = kFPrio | kFClsAhead | kFSpread | kFReadsValu;  // round 2: c3 forward 2.53 -> 2.38 ms
 constexpr int kADma = 131072;  // ablation (results wrong: no ordering): staging by LDS-DMA in place of load + store
 constexpr int kFLoadsValu = 65536;  // staging loads issued in the softmax phase (no memory traffic otherwise)
 constexpr int kFStampFine = 8;  // diagnostic: with kFStamp, also stamp the parts of the MFMA phase
@@ -302,10 +304,24 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
   // softmax of tile `it` (see fa_fwd_f16_pingpong.hip); the scores are first moved to the running
   // reference m_run (at this d the VALU phase has room for the subtraction)
   auto softmax = [&](int it, int cls) __attribute__((always_inline)) {
+    if constexpr ((F & kFPkSub) != 0) {
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 nm = {-m_run, -m_run};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      st[0][i] -= m_run;
-      st[1][i] -= m_run;
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          f2 x = {st[t][i], st[t][i + 1]};
+          x += nm;
+          st[t][i] = x[0];
+          st[t][i + 1] = x[1];
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        st[0][i] -= m_run;
+        st[1][i] -= m_run;
+      }
     }
     if (cls == 1) mask(tk0(it));
     float mx[4];
@@ -473,11 +489,13 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
     // this phase's stores are complete before its barrier: the other group reads K(i+2) / V(i+1)
     // at the end of the next interval (the reads above were already waited for by the MFMAs)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    if constexpr ((F & kFEarlyKQ) == 0) {
-      read_k((c + 1) % kNS, 0);
-      read_q(0);
+    if constexpr ((F & kFReadsValu) == 0) {
+      if constexpr ((F & kFEarlyKQ) == 0) {
+        read_k((c + 1) % kNS, 0);
+        read_q(0);
+      }
+      read_v(c, 0);
     }
-    read_v(c, 0);
     if (F & kFPrio) __builtin_amdgcn_s_setprio(0);
   };
   // The pipelined MFMA phase (kFPipe): the 32 MFMAs run unconditionally (P is zero for a skipped
@@ -567,7 +585,15 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
     __builtin_amdgcn_s_waitcnt(0xC67F);  // lgkmcnt(6)
     if (F & kFPrio) __builtin_amdgcn_s_setprio(0);
   };
-  auto valu_phase = [&](int it) __attribute__((always_inline)) {
+  auto valu_phase = [&](auto C_, int it) __attribute__((always_inline)) {
+    if constexpr ((F & kFReadsValu) != 0) {
+      // K(i+1) / V(i) were published before MFMA(i) began; this interval's stores (the other
+      // group's MFMA phase) go to the K(i-1) / V(i-2) slots
+      constexpr int c = decltype(C_)::value;
+      read_k((c + 1) % kNS, 0);
+      read_q(0);
+      read_v(c, 0);
+    }
     if constexpr ((F & kFLoadsValu) != 0) {  // the tiles this group stores at the start of MFMA(it+1)
       load(kst, krs, koff, tk0(it + 3));
       load(vst, vrs, voff, tk0(it + 2));
@@ -615,7 +641,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong128_kernel(FwdArg
     stamp(1);
     __builtin_amdgcn_s_barrier();
     stamp(2);
-    valu_phase(it);
+    valu_phase(C_, it);
     stamp(3);
     if constexpr ((F & kFStamp) != 0) st_acc[4] += 1;
   };
@@ -727,6 +753,10 @@ hipError_t launch_fwd_f16_pingpong128(const FwdArgs& a, hipStream_t s) {
     case 2358: return launch_t<kFPrio | kFClsAhead>(a, s);
     case 2359: return launch_t<kFPrio | kFClsAhead | kFStamp | kFStampFine>(a, s);
     case 2360: return launch_t<kFPrio | kFClsAhead | kFSpread>(a, s);
+    case 2362: return launch_t<kFDefault | kFPkSub>(a, s);
+    case 2365: return launch_t<(kFDefault & ~kFReadsValu)>(a, s);  // before the reads moved to the softmax phase
+    case 2363: return launch_t<kFDefault | kFReadsValu | kFStamp | kFStampFine>(a, s);
+    case 2364: return launch_t<kFDefault | kFStamp | kFStampFine>(a, s);
     case 2310: return launch_t<kFPrio | kFPipe>(a, s);
     case 2311: return launch_t<kFPrio | kFPipe | kFStamp>(a, s);
     case 2312: return launch_t<kFPipe>(a, s);
