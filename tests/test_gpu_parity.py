@@ -386,6 +386,20 @@ def test_config5_full2d_f32_sampled():
 #   staging pinned too; forced here for causal / local, where the interleave is off), 2212
 #   ping-pong with LDS-DMA staging, 1814 the 8-wave forward that the ping-pong kernel replaced, and
 #   bwd 1281 the software-pipelined dK/dV pass (d = 128).
+@pytest.fixture
+def diag_lib(monkeypatch):
+    """Routes the test through the diagnostic library (libfa_hip_diag.so), where the variant
+    selectors exist; the product library has none and would silently run its default.  The diag
+    library must have been built from the current sources (its build info carries their hash)."""
+    from tf_flash_attention_amd import _lib
+    if not __import__("os").path.exists(_lib.DIAG_LIB_PATH):
+        pytest.skip("libfa_hip_diag.so not built (make -C tf_flash_attention_amd diag)")
+    with _lib.using(_lib.DIAG_LIB_PATH):
+        info = _lib.build_info()
+        assert "lib=diag" in info and f"src={_lib.source_hash()};" in info, info
+        yield
+
+
 VARIANT_CASES = [
     ("full", 1, "none_front", (264,), (136,), 1, False, 64, 64),
     ("full", 1, "none_front", (300,), (1000,), 1, False, 48, 64),
@@ -399,7 +413,7 @@ VARIANT_CASES = [
 
 @pytest.mark.parametrize("variant", ["2000", "2200", "2201", "2206", "2207", "2208", "2212", "2213", "1814"])
 @pytest.mark.parametrize("policy,seq_dims,mode,qs,ks,ws,causal,d,vd", VARIANT_CASES)
-def test_f16_forward_structures(monkeypatch, variant, policy, seq_dims, mode, qs, ks, ws, causal, d, vd):
+def test_f16_forward_structures(monkeypatch, diag_lib, variant, policy, seq_dims, mode, qs, ks, ws, causal, d, vd):
     monkeypatch.setenv("FA_FWD_VARIANT", variant)
     run_case(np.float16, policy, seq_dims, mode, (2, 2), d, vd, qs, ks, ws=ws, ls=0, causal=causal, bwd=False,
              seed=int(variant) + d + ws)
@@ -407,7 +421,7 @@ def test_f16_forward_structures(monkeypatch, variant, policy, seq_dims, mode, qs
 
 @pytest.mark.parametrize("variant", ["2300", "2301", "2399", "146"])
 @pytest.mark.parametrize("policy,seq_dims,mode,qs,ks,ws,causal,d,vd", VARIANT_CASES)
-def test_f16_forward_structures_d128(monkeypatch, variant, policy, seq_dims, mode, qs, ks, ws, causal, d, vd):
+def test_f16_forward_structures_d128(monkeypatch, diag_lib, variant, policy, seq_dims, mode, qs, ks, ws, causal, d, vd):
     """d in (64, 128]: the ping-pong kernel (2300 no priority flips, 2301 the default, 2399 staging at the
     MFMA-phase head; forced for local too) and the 4-wave kernel (146)."""
     monkeypatch.setenv("FA_FWD_VARIANT", variant)
@@ -419,13 +433,13 @@ def test_f16_forward_structures_d128(monkeypatch, variant, policy, seq_dims, mod
 # default before the run-ahead reads), 1069 = the d <= 64 passes with run-ahead reads
 @pytest.mark.parametrize("variant,d", [("1200", 128), ("1069", 64), ("1069", 48)])
 @pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, True)])
-def test_f16_backward_read_placement(monkeypatch, variant, d, policy, ws, causal):
+def test_f16_backward_read_placement(monkeypatch, diag_lib, variant, d, policy, ws, causal):
     monkeypatch.setenv("FA_BWD_VARIANT", variant)
     run_case(np.float16, policy, 1, "none_front", (2,), d, d, (328,), (264,), ws=ws, ls=0, causal=causal,
              seed=int(variant) + d)
 
 
 @pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, False)])
-def test_f16_backward_pipelined_dkdv(monkeypatch, policy, ws, causal):
+def test_f16_backward_pipelined_dkdv(monkeypatch, diag_lib, policy, ws, causal):
     monkeypatch.setenv("FA_BWD_VARIANT", "1281")
     run_case(np.float16, policy, 1, "none_front", (2,), 128, 128, (328,), (264,), ws=ws, ls=0, causal=causal, seed=7)

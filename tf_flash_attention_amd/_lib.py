@@ -7,6 +7,7 @@ CPU fallback.  If the HIP library is missing the first call raises
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -63,6 +64,9 @@ class FaProblem(ctypes.Structure):
 
 _lock = threading.Lock()
 _lib = None
+_override = None  # a library routed in by using() (tests: the diagnostic build's variants)
+_loaded = {}
+DIAG_LIB_PATH = os.path.join(_HERE, "libfa_hip_diag.so")
 
 
 def _declare(lib):
@@ -99,6 +103,8 @@ def _declare(lib):
 def lib():
     """Load (once) and return the HIP library, or raise LibraryNotBuiltError."""
     global _lib
+    if _override is not None:
+        return _override
     if _lib is not None:
         return _lib
     with _lock:
@@ -112,6 +118,27 @@ def lib():
             except OSError as e:  # pragma: no cover - environment problem
                 raise LibraryNotBuiltError(f"failed to load {LIB_PATH}: {e}") from e
     return _lib
+
+
+@contextlib.contextmanager
+def using(path):
+    """Route every call made inside the block through the library at ``path``.
+
+    The GPU tests use it to run the diagnostic build (libfa_hip_diag.so, ``make -C
+    tf_flash_attention_amd diag``): its FA_FWD_VARIANT / FA_BWD_VARIANT structures are not in
+    the product library.  ctypes loads each library RTLD_LOCAL, so both can live in one process."""
+    global _override
+    with _lock:
+        h = _loaded.get(path)
+        if h is None:
+            if not os.path.exists(path):
+                raise LibraryNotBuiltError(f"library not found at {path}")
+            h = _loaded[path] = _declare(ctypes.CDLL(path))
+    prev, _override = _override, h
+    try:
+        yield h
+    finally:
+        _override = prev
 
 
 def make_problem(dtype, policy, seq_dims, sync_mode, b, q_seq, k_seq, d, v_d,
