@@ -419,19 +419,21 @@ def test_f16_forward_structures(monkeypatch, diag_lib, variant, policy, seq_dims
              seed=int(variant) + d + ws)
 
 
-@pytest.mark.parametrize("variant", ["2300", "2301", "2399", "146"])
+@pytest.mark.parametrize("variant", ["2300", "2301", "2340", "2362", "2399", "146"])
 @pytest.mark.parametrize("policy,seq_dims,mode,qs,ks,ws,causal,d,vd", VARIANT_CASES)
 def test_f16_forward_structures_d128(monkeypatch, diag_lib, variant, policy, seq_dims, mode, qs, ks, ws, causal, d, vd):
-    """d in (64, 128]: the ping-pong kernel (2300 no priority flips, 2301 the default, 2399 staging at the
-    MFMA-phase head; forced for local too) and the 4-wave kernel (146)."""
+    """d in (64, 128]: the ping-pong kernel (2300 no priority flips, 2301 the default, 2340 key tiles from
+    staggered starts, 2362 packed-fp32 reference subtraction, 2399 staging at the MFMA-phase head;
+    forced for local too) and the 4-wave kernel (146)."""
     monkeypatch.setenv("FA_FWD_VARIANT", variant)
     run_case(np.float16, policy, seq_dims, mode, (2, 2), d + 64, vd + 32, qs, ks, ws=ws, ls=0, causal=causal,
              bwd=False, seed=int(variant) + d + ws)
 
 
 # backward operand-read placement: 1200 = the d = 128 passes with reads beside their MFMAs (the
-# default before the run-ahead reads), 1069 = the d <= 64 passes with run-ahead reads
-@pytest.mark.parametrize("variant,d", [("1200", 128), ("1069", 64), ("1069", 48)])
+# default before the run-ahead reads), 1500 / 1501 = the dQ pass's staging (stores and loads / loads
+# only) spread over its MFMA pairs, 1069 = the d <= 64 passes with run-ahead reads
+@pytest.mark.parametrize("variant,d", [("1200", 128), ("1500", 128), ("1501", 128), ("1069", 64), ("1069", 48)])
 @pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, True)])
 def test_f16_backward_read_placement(monkeypatch, diag_lib, variant, d, policy, ws, causal):
     monkeypatch.setenv("FA_BWD_VARIANT", variant)
