@@ -492,7 +492,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 // producer, the dK / dV accumulators in the consumer, each role inside its own loop so neither
 // carries the other's registers (under 256 each at D = 128).  Every step: one barrier, the
 // staging of tile i+1 into the ring, the load of tile i+3.
-template <int D>
+template <int D, bool SMX = false>
 struct PcSmem {
   static constexpr int kBK = 128;            // keys per workgroup: four producer waves x 32
   static constexpr int kRow = D * kBK * 2;   // K (or V) row image (prologue only)
@@ -501,7 +501,8 @@ struct PcSmem {
   static constexpr int kSlot = offLse + 2 * 32 * 4;  // + -lse2[32], -D[32]
   static constexpr int kNS = 4;              // query-tile ring
   static constexpr int offX = kNS * kSlot;   // P / dS hand-over: 2 slots x 4 waves x 4 KB
-  static constexpr int kXSlot = 4 * 4096;
+  static constexpr int kXWave = SMX ? 8192 : 4096;  // (SMX: raw fp32 S and dP, 8 KB a wave)
+  static constexpr int kXSlot = 4 * kXWave;
   static constexpr int kUsed = offX + 2 * kXSlot;
   static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;  // the K/V images alias the ring
 };
@@ -510,7 +511,10 @@ template <int D, int POL, bool ALN, int PF = 0>
 __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
-  using S = PcSmem<D>;
+  // PF & 64 (SMX): the producer hands over its raw fp32 S and dP; the consumer, which otherwise
+  // waits at the barrier for about half of each step, forms P = exp2(S) and dS = P∘dP itself
+  constexpr bool SMX = (PF & 64) != 0;
+  using S = PcSmem<D, SMX>;
   constexpr int kThr = 512;
   constexpr int kBK = S::kBK;
   constexpr int kQChunks = D * 4;                 // 16-B chunks of one [D][32] tile
@@ -659,7 +663,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
     if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr[set];
   };
   // hand-over slot of this wave pair: four b128 per lane (P k-steps 0/1, dS k-steps 0/1), lane-linear
-  auto xoff = [&](int xs, int j) -> uint32_t { return S::offX + xs * S::kXSlot + wl * 4096 + j * 1024 + lane * 16; };
+  auto xoff = [&](int xs, int j) -> uint32_t { return S::offX + xs * S::kXSlot + wl * S::kXWave + j * 1024 + lane * 16; };
 
   // Steps it = 0 .. ntiles: the producer handles tile it (it < ntiles), the consumer tile it-1 (it >= 1).
   // Whole groups of four steps (ring slot it % 4, staging set (it+1) % 2, hand-over slot it % 2 are
@@ -721,7 +725,8 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
           }
         }
         // S = Qᵀ·K', dP = dOᵀ·V: A operands by transposed reads, two k-steps ahead of their MFMAs
-        constexpr int kS = D / 16, kAh = 2;
+        // (PF & 128: four ahead)
+        constexpr int kS = D / 16, kAh = (PF & 128) ? 4 : 2;
         half8 qa8[kAh + 1], oa8[kAh + 1];
         auto rd = [&](int s_) __attribute__((always_inline)) {
 #pragma unroll
@@ -746,6 +751,15 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       stamp(1);
       if constexpr (TWO) __builtin_amdgcn_s_barrier();  // phase B: this softmax beside the consumer's MFMAs
       if (cls == 0) return;
+      if constexpr (SMX) {  // raw S (chunks 0-3) and dP (4-7), four registers a chunk, lane-linear
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          *reinterpret_cast<lds_f4_t*>(smem + xoff(c % 2, j)) = floatx4{sacc[4 * j], sacc[4 * j + 1], sacc[4 * j + 2], sacc[4 * j + 3]};
+          *reinterpret_cast<lds_f4_t*>(smem + xoff(c % 2, 4 + j)) = floatx4{pacc[4 * j], pacc[4 * j + 1], pacc[4 * j + 2], pacc[4 * j + 3]};
+        }
+        stamp(2);
+        return;
+      }
       // P = exp2(S), dS = P∘dP; register i = query 16(i>>3) + 8h + (i&7) = k-step i>>3 of the consumer
       half8 pf[2], sf[2];
 #pragma unroll
@@ -780,6 +794,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   }
 
   // ================= consumer
+  const int kord = (POL == 2 && SMX) ? seq_order(a.rule.k, a.rule, min(key, nk - 1)) : 0;
   stage0();
   floatx16 dk[D / 32], dv[D / 32];
 #pragma unroll
@@ -802,11 +817,36 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       oa[n % (kAh + 1)] = read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s_ + h));
       qa_[n % (kAh + 1)] = read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s_ + h));
     };
-    if (cls != 0) {
+    // SMX: P and dS of k-step s_ (registers i = 8 s_ + jj of the producer's S / dP) formed here
+    auto smx = [&](int s_) __attribute__((always_inline)) {
+      const int xs = (c + 1) % 2;
+      const floatx4 s0 = *reinterpret_cast<const lds_f4_t*>(smem + xoff(xs, 2 * s_));
+      const floatx4 s1 = *reinterpret_cast<const lds_f4_t*>(smem + xoff(xs, 2 * s_ + 1));
+      const floatx4 d0 = *reinterpret_cast<const lds_f4_t*>(smem + xoff(xs, 4 + 2 * s_));
+      const floatx4 d1 = *reinterpret_cast<const lds_f4_t*>(smem + xoff(xs, 5 + 2 * s_));
 #pragma unroll
-      for (int s_ = 0; s_ < 2; ++s_) {
-        pf[s_] = read_b128(smem + xoff((c + 1) % 2, s_));
-        sf[s_] = read_b128(smem + xoff((c + 1) % 2, 2 + s_));
+      for (int jj = 0; jj < 8; ++jj) {
+        const float sv = jj < 4 ? s0[jj] : s1[jj - 4], dpv = jj < 4 ? d0[jj] : d1[jj - 4];
+        float pv = __builtin_amdgcn_exp2f(sv);
+        if (POL == 1 && cls == 1) {
+          const int q = qa + 16 * s_ + 8 * h + jj;
+          pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
+        }
+        if (POL == 2 && cls == 1) {
+          const int q = qa + 16 * s_ + 8 * h + jj;
+          pv = (q < nq && check_orders_bf(a.rule, seq_order(a.rule.q, a.rule, min(q, nq - 1)), kord)) ? pv : 0.f;
+        }
+        pf[s_][jj] = (_Float16)pv;
+        sf[s_][jj] = (_Float16)(pv * dpv);
+      }
+    };
+    if (cls != 0) {
+      if constexpr (!SMX) {
+#pragma unroll
+        for (int s_ = 0; s_ < 2; ++s_) {
+          pf[s_] = read_b128(smem + xoff((c + 1) % 2, s_));
+          sf[s_] = read_b128(smem + xoff((c + 1) % 2, 2 + s_));
+        }
       }
 #pragma unroll
       for (int n = 0; n < kAh; ++n) rd(n);
@@ -814,8 +854,12 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
     stamp(1);
     if constexpr (TWO) __builtin_amdgcn_s_barrier();  // phase B: these MFMAs beside the producer's softmax
     if (cls == 0) return;
+    if constexpr (SMX) smx(0);
 #pragma unroll
     for (int n = 0; n < kN; ++n) {
+      if constexpr (SMX) {
+        if (n == 1) smx(1);  // k-step 1's P / dS beside k-step 0's MFMAs
+      }
       if (n + kAh < kN) rd(n + kAh);
       const int s_ = n / kU, u = n % kU;
       dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa[n % (kAh + 1)], pf[s_], dv[u], 0, 0, 0);
@@ -1210,7 +1254,7 @@ hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
 
 template <int D, int PF = 0>
 hipError_t launch_dkdv_pc(const BwdArgs& a, hipStream_t s) {
-  using S = PcSmem<D>;
+  using S = PcSmem<D, (PF & 64) != 0>;
   const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
   const int pol = bwd_pol(a.rule);
   const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dkdv_pc_kernel<D, 0, true, PF>
@@ -1285,6 +1329,11 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
       case 1403: e = launch_dkdv_pc<128, 3>(a, s); break;
       case 1404: e = launch_dkdv_pc<128, 4>(a, s); break;  // stamps into the dQ workspace (tools/pc_stamps.py)
       case 1406: e = launch_dkdv_pc<128, 6>(a, s); break;
+      case 1410: e = launch_dkdv_pc<128, 64>(a, s); break;  // the softmax on the consumer side
+      case 1411: e = launch_dkdv_pc<128, 64 | 4>(a, s); break;
+      case 1412: e = launch_dkdv_pc<128, 64 | 1>(a, s); break;
+      case 1413: e = launch_dkdv_pc<128, 128>(a, s); break;  // producer operand reads four k-steps ahead
+      case 1414: e = launch_dkdv_pc<128, 128 | 4>(a, s); break;
       case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
       case 1200: e = launch_dkdv<128, 4, 1>(a, s); break;  // operand reads not run ahead (before the default)
       case 1264: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
