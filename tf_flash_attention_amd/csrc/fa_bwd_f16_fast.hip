@@ -762,19 +762,32 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       }
       // P = exp2(S), dS = P∘dP; register i = query 16(i>>3) + 8h + (i&7) = k-step i>>3 of the consumer
       half8 pf[2], sf[2];
+      auto softmax = [&](bool masked) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float pv = __builtin_amdgcn_exp2f(sacc[i]);
-        if (POL == 1 && cls == 1) {
-          const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
-          pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
+        for (int i = 0; i < 16; ++i) {
+          float pv = __builtin_amdgcn_exp2f(sacc[i]);
+          if (POL == 1 && masked) {
+            const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
+            pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
+          }
+          if (POL == 2 && masked) {
+            const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
+            pv = (q < nq && check_orders_bf(a.rule, seq_order(a.rule.q, a.rule, min(q, nq - 1)), ko)) ? pv : 0.f;
+          }
+          pf[i >> 3][i & 7] = (_Float16)pv;
+          sf[i >> 3][i & 7] = (_Float16)(pv * pacc[i]);
         }
-        if (POL == 2 && cls == 1) {
-          const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
-          pv = (q < nq && check_orders_bf(a.rule, seq_order(a.rule.q, a.rule, min(q, nq - 1)), ko)) ? pv : 0.f;
-        }
-        pf[i >> 3][i & 7] = (_Float16)pv;
-        sf[i >> 3][i & 7] = (_Float16)(pv * pacc[i]);
+      };
+      // the edge-tile mask as a real branch: in one basic block hipcc if-converts it into an index add,
+      // a compare and two selects per score on every tile (PF & 256: that form, for A/B)
+      if constexpr ((PF & 256) != 0) {
+        softmax(cls == 1);
+      } else if (POL != 0 && cls == 1) {
+        asm volatile("; edge tile" ::: );
+        softmax(true);
+      } else {
+        asm volatile("; interior tile" ::: );
+        softmax(false);
       }
 #pragma unroll
       for (int s_ = 0; s_ < 2; ++s_) {
@@ -1515,12 +1528,24 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
           const floatx16 st = half_chain(base + S::offKT, qf, negl, t);
           const floatx16 dp = half_chain(base + S::offVT, of, negd, t);
           if constexpr ((PF & 1) != 0) __builtin_amdgcn_s_setprio(0);
+          auto softmax = [&](int cl) __attribute__((always_inline)) {
 #pragma unroll
-          for (int sh = 0; sh < 2; ++sh) {
-            half8 dsf;
+            for (int sh = 0; sh < 2; ++sh) {
+              half8 dsf;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) dsf[j] = (_Float16)(pval(st[8 * sh + j], cls, ka, t, 8 * sh + j) * dp[8 * sh + j]);
-            *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, 2 * t + sh)) = dsf;
+              for (int j = 0; j < 8; ++j) dsf[j] = (_Float16)(pval(st[8 * sh + j], cl, ka, t, 8 * sh + j) * dp[8 * sh + j]);
+              *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, 2 * t + sh)) = dsf;
+            }
+          };
+          // the edge-tile mask as a real branch (see the dK/dV pass; PF & 8: the if-converted form)
+          if constexpr ((PF & 8) != 0) {
+            softmax(cls);
+          } else if (cls == 1) {
+            asm volatile("; edge tile" ::: );
+            softmax(1);
+          } else {
+            asm volatile("; interior tile" ::: );
+            softmax(2);
           }
         }
       };
@@ -1746,6 +1771,8 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
       case 1411: e = launch_dkdv_pc<128, 64 | 4>(a, s); break;
       case 1412: e = launch_dkdv_pc<128, 64 | 1>(a, s); break;
       case 1413: e = launch_dkdv_pc<128, 128>(a, s); break;  // producer operand reads four k-steps ahead
+      case 1420: e = launch_dkdv_pc<128, 256>(a, s); break;  // the edge mask if-converted (before)
+      case 1421: e = launch_dkdv_pc<128, 256>(a, s); break;  // (with 1608's dQ pass)
       case 1414: e = launch_dkdv_pc<128, 128 | 4>(a, s); break;
       case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
       case 1200: e = launch_dkdv<128, 4, 1>(a, s); break;  // operand reads not run ahead (before the default)
@@ -1769,6 +1796,8 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
     if (v == 1600) return launch_dq_pc<128>(a, s);  // producer / consumer dQ pass
     if (v == 1601) return launch_dq_pc<128, 1>(a, s);  // ... the producer's MFMAs at priority 1
     if (v == 1604) return launch_dq_pc<128, 4>(a, s);  // ... dPᵀ / dSᵀ formed by the consumer
+    if (v == 1608) return launch_dq_pc<128, 8>(a, s);  // ... the edge mask if-converted (before)
+    if (v == 1421) return launch_dq_pc<128, 8>(a, s);
     if (bwd_aligned(a)) return launch_dq_pc<128>(a, s);
     return launch_dq<128, 4, 1, true>(a, s);
   }
