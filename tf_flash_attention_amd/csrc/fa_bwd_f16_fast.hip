@@ -325,20 +325,33 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
     }
   };
   // P = exp2(S), dS = P∘dP; k-step s of the dV / dK products = registers 8s..8s+7
-  auto softmax = [&](const floatx16& sacc, const floatx16& pacc, int qa, int cls, half8 (&pf)[2], half8 (&sf)[2]) {
+  auto softmax_m = [&](const floatx16& sacc, const floatx16& pacc, int qa, bool masked, half8 (&pf)[2], half8 (&sf)[2])
+      __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float pv = (ABL & 1) ? sacc[i] : __builtin_amdgcn_exp2f(sacc[i]);
-      if (POL == 1 && cls == 1) {
+      if (POL == 1 && masked) {
         const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
         pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
       }
-      if (POL == 2 && cls == 1) {
+      if (POL == 2 && masked) {
         const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
         pv = (q < nq && check_orders_bf(a.rule, seq_order(a.rule.q, a.rule, min(q, nq - 1)), ko)) ? pv : 0.f;
       }
       pf[i >> 3][i & 7] = (_Float16)pv;
       sf[i >> 3][i & 7] = (_Float16)(pv * pacc[i]);
+    }
+  };
+  // the edge-tile mask as a real branch (see the producer / consumer pass; ABL & 512: the if-converted form)
+  auto softmax = [&](const floatx16& sacc, const floatx16& pacc, int qa, int cls, half8 (&pf)[2], half8 (&sf)[2]) {
+    if constexpr ((ABL & 512) != 0 || POL == 0) {
+      softmax_m(sacc, pacc, qa, cls == 1, pf, sf);
+    } else if (cls == 1) {
+      asm volatile("; edge tile" ::: );
+      softmax_m(sacc, pacc, qa, true, pf, sf);
+    } else {
+      asm volatile("; interior tile" ::: );
+      softmax_m(sacc, pacc, qa, false, pf, sf);
     }
   };
   // dV += dO·P, dK += Q·dS: A = X[row 32u + r][queries 16s + 8h + 0..7] (b128 reads of the Q16 images)
@@ -929,7 +942,7 @@ struct DqSmem {
 };
 
 // dQ: query-outer.  One workgroup = NW waves x 32 queries of one (batch, head) slice.
-template <int D, int NW, int WPE, int POL, bool ALN, bool PRE = false, int SPR = 0>
+template <int D, int NW, int WPE, int POL, bool ALN, bool PRE = false, int SPR = 0, bool MSPEC = false>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -1179,6 +1192,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
         dp[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, of[s], s == 0 ? negd : dp[t], 0, 0, 0);
       }
     // dSᵀ = exp2(Sᵀ)∘dPᵀ; keys of register i of half t: 32t + 16(i>>3) + 8h + (i&7)
+    auto dsq = [&](int cl) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       half8 dsf;
@@ -1186,7 +1200,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
       for (int j = 0; j < 8; ++j) {
         const int t = s >> 1, i = 8 * (s & 1) + j;
         float pv = __builtin_amdgcn_exp2f(st[t][i]);
-        if (cls == 1) {
+        if (cl == 1) {
           const int kk = ka + 32 * t + 16 * (i >> 3) + 8 * h + (i & 7);
           const bool ok = (POL == 1)   ? ((unsigned)(kk - klo) < (unsigned)kspan)
                           : (POL == 2) ? (kk < nk && check_orders_bf(a.rule, qo, seq_order(a.rule.k, a.rule, min(kk, nk - 1))))
@@ -1206,6 +1220,17 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
           dq[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka8, dsf, dq[u], 0, 0, 0);
         }
       }
+    }
+    };
+    // the edge-tile mask as a real branch (see the producer / consumer pass; MSPEC: the if-converted form)
+    if constexpr (MSPEC) {
+      dsq(cls);
+    } else if (cls == 1) {
+      asm volatile("; edge tile" ::: );
+      dsq(1);
+    } else {
+      asm volatile("; interior tile" ::: );
+      dsq(2);
     }
   };
   for (int it = 0; it < ntiles; it += 2) {  // whole pairs (see the dK/dV pass)
@@ -1690,17 +1715,17 @@ hipError_t launch_dkdv_pc(const BwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int D, int NW, int WPE, bool PRE = false, int SPR = 0>
+template <int D, int NW, int WPE, bool PRE = false, int SPR = 0, bool MSPEC = false>
 hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
   using S = DqSmem<D, NW>;
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
   const int pol = bwd_pol(a.rule);
-  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, true, PRE, SPR>
-                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, true, PRE, SPR>
-                                                      : bwd_dq_kernel<D, NW, WPE, 2, true, PRE, SPR>)
-                                        : (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, false, PRE, SPR>
-                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, false, PRE, SPR>
-                                                      : bwd_dq_kernel<D, NW, WPE, 2, false, PRE, SPR>);
+  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, true, PRE, SPR, MSPEC>
+                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, true, PRE, SPR, MSPEC>
+                                                      : bwd_dq_kernel<D, NW, WPE, 2, true, PRE, SPR, MSPEC>)
+                                        : (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, false, PRE, SPR, MSPEC>
+                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, false, PRE, SPR, MSPEC>
+                                                      : bwd_dq_kernel<D, NW, WPE, 2, false, PRE, SPR, MSPEC>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(NW * 64), S::kTotal, s, a);
@@ -1748,14 +1773,16 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   if (max(a.d, a.v_d) <= 64 && v >= 0) {
     switch (v) {
       case 82: e = launch_dkdv<64, 8, 2>(a, s); break;
+      case 1070: e = launch_dkdv<64, 4, 2, false, 512>(a, s); break;  // the edge mask if-converted (before)
       case 1067: case 1069: e = launch_dkdv<64, 4, 2, false, 64>(a, s); break;
       default: e = launch_dkdv<64, 4, 2>(a, s); break;
     }
     if (e != hipSuccess) return e;
     switch (v) {
-      case 82: return launch_dq<64, 8, 2>(a, s);
+      case 82: return launch_dq<64, 8, 2, false, 0, true>(a, s);
       case 1068: case 1069: return launch_dq<64, 4, 2, true>(a, s);
-      default: return launch_dq<64, 4, 2>(a, s);
+      case 1071: return launch_dq<64, 4, 2>(a, s);  // the dQ pass with the edge-mask branch (spills)
+      default: return launch_dq<64, 4, 2, false, 0, true>(a, s);
     }
   }
   if (max(a.d, a.v_d) > 64 && v >= 0) {
@@ -1805,7 +1832,8 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   if (max(a.d, a.v_d) <= 64) {
     e = launch_dkdv<64, 4, 2>(a, s);
     if (e != hipSuccess) return e;
-    return launch_dq<64, 4, 2>(a, s);
+    // (the d <= 64 dQ pass keeps the if-converted edge mask: the branch form spills 8-42 VGPRs there)
+    return launch_dq<64, 4, 2, false, 0, true>(a, s);
   }
   // tuned (c3): the producer / consumer dK/dV pass (one-process A/B: 9.20 -> 8.59 ms backward; two
   // barriers per step, 1402, and a prioritised producer, 1401, measured 8.70 / 8.77) and, for 16-B
