@@ -433,11 +433,11 @@ def test_f16_forward_structures_d128(monkeypatch, diag_lib, variant, policy, seq
 # backward operand-read placement: 1200 = the d = 128 passes with reads beside their MFMAs (the
 # default before the run-ahead reads), 1410 = the dK/dV pass with P / dS formed by the consumer
 # waves, 1413 = its producer reading operands four k-steps ahead, 1500 / 1501 = the dQ pass's
-# staging (stores and loads / loads only) spread over its MFMA pairs, 1599 = the one-wave dQ pass, 1600 / 1601 / 1604 = the producer / consumer dQ pass, 1421 = both producer / consumer passes with the if-converted edge mask
+# staging (stores and loads / loads only) spread over its MFMA pairs, 1599 = the one-wave dQ pass, 1600 / 1601 / 1604 = the producer / consumer dQ pass, 1421 = both producer / consumer passes with the if-converted edge mask, 1430 = the dK/dV producer pre-reading the next tile
 # dQ pass, 1070 / 1071 = the d <= 64 passes with the if-converted edge mask / the dQ branch form, 1069 = the d <= 64 passes
 # with run-ahead reads
 @pytest.mark.parametrize("variant,d", [("1200", 128), ("1410", 128), ("1413", 128), ("1500", 128), ("1501", 128),
-                                       ("1599", 128), ("1600", 128), ("1601", 128), ("1604", 128), ("1421", 128), ("1069", 64), ("1069", 48), ("1070", 64), ("1071", 64)])
+                                       ("1599", 128), ("1600", 128), ("1601", 128), ("1604", 128), ("1421", 128), ("1430", 128), ("1069", 64), ("1069", 48), ("1070", 64), ("1071", 64)])
 @pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, True)])
 def test_f16_backward_read_placement(monkeypatch, diag_lib, variant, d, policy, ws, causal):
     monkeypatch.setenv("FA_BWD_VARIANT", variant)

@@ -683,19 +683,35 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   // compile-time); loads and stores are unconditional (phantom tiles move zeros), so hipcc's vmcnt
   // waits stay exact.
   const int nsteps = ntiles + 1;
+  // PF & 512 (AHD): tiles stored two steps ahead (tile it+2 in step it, loads four ahead), so the
+  // producer reads the next tile's row constants and first operands before the step's barrier
+  constexpr bool AHD = (PF & 512) != 0;
   auto stage = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;
     __syncthreads();
-    store_tile((c + 1) % 4, (c + 1) % 2);           // tile it+1 (loaded in step it-2)
-    load_tile(qt0 + 32 * (it + 3), (c + 1) % 2);    // tile it+3 into the set just stored
+    if constexpr (AHD) {
+      store_tile((c + 2) % 4, c % 2);               // tile it+2 (loaded in step it-2)
+      load_tile(qt0 + 32 * (it + 4), c % 2);        // tile it+4 into the set just stored
+    } else {
+      store_tile((c + 1) % 4, (c + 1) % 2);         // tile it+1 (loaded in step it-2)
+      load_tile(qt0 + 32 * (it + 3), (c + 1) % 2);  // tile it+3 into the set just stored
+    }
   };
   // first tiles: tile 0's loads issued now, its store after the barrier that retires the K/V images
   load_tile(qt0, 0);
+  if constexpr (AHD) load_tile(qt0 + 32, 1);
   auto stage0 = [&]() __attribute__((always_inline)) {
     __syncthreads();
     store_tile(0, 0);
-    load_tile(qt0 + 32, 1);
-    load_tile(qt0 + 64, 0);
+    if constexpr (AHD) {
+      store_tile(1, 1);
+      load_tile(qt0 + 64, 0);
+      load_tile(qt0 + 96, 1);
+      __syncthreads();  // tiles 0 and 1 published: the producer pre-reads tile 0
+    } else {
+      load_tile(qt0 + 32, 1);
+      load_tile(qt0 + 64, 0);
+    }
   };
 
   if (grp == 0) {
@@ -716,6 +732,42 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every image read done before the ring reuses it
     stage0();
     const int ko = (POL == 2) ? seq_order(a.rule.k, a.rule, min(key, nk - 1)) : 0;
+    // row constants (-lse2, -D) of a tile: registers 4gq..4gq+3 = queries 16(gq>>1) + 8h + 4(gq&1) + 0..3
+    auto read_rowc = [&](const lds_char_t* base, floatx16& sa, floatx16& pa) __attribute__((always_inline)) {
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int q4 = 16 * (gq >> 1) + 8 * h + 4 * (gq & 1);
+        const floatx4 l4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 4 * q4);
+        const floatx4 d4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 128 + 4 * q4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sa[4 * gq + j] = l4[j];
+          pa[4 * gq + j] = d4[j];
+        }
+      }
+    };
+    // the S / dP A operands of k-step s_ (transposed reads of the Q16 images)
+    auto read_ops = [&](const lds_char_t* base, int s_, half8& q8, half8& o8) __attribute__((always_inline)) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const uint32_t off = q16_off(16 * s_ + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
+        const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
+        if (e == 0) { q8.lo = x; o8.lo = y; } else { q8.hi = x; o8.hi = y; }
+      }
+    };
+    floatx16 nsacc, npacc;  // AHD: the next tile's row constants and first two k-steps' operands
+    half8 nq8[2], no8[2];
+    auto preread = [&](int slot, int itn) __attribute__((always_inline)) {
+      if constexpr (AHD) {
+        const int cl = itn < ntiles ? tcls(qt0 + 32 * itn) : 0;
+        if (cl == 0) return;
+        const lds_char_t* base = smem + slot * S::kSlot;
+        read_rowc(base, nsacc, npacc);
+#pragma unroll
+        for (int s_ = 0; s_ < 2; ++s_) read_ops(base, s_, nq8[s_], no8[s_]);
+      }
+    };
+    preread(0, 0);
     auto pstep = [&](auto C_, int it) __attribute__((always_inline)) {
       constexpr int c = decltype(C_)::value;
       stamp(-1);
@@ -726,32 +778,23 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       const lds_char_t* base = smem + c * S::kSlot;
       floatx16 sacc, pacc;
       if (cls != 0) {
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {  // registers 4gq..4gq+3 = queries 16(gq>>1) + 8h + 4(gq&1) + 0..3
-          const int q4 = 16 * (gq >> 1) + 8 * h + 4 * (gq & 1);
-          const floatx4 l4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 4 * q4);
-          const floatx4 d4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 128 + 4 * q4);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            sacc[4 * gq + j] = l4[j];
-            pacc[4 * gq + j] = d4[j];
-          }
-        }
         // S = Qᵀ·K', dP = dOᵀ·V: A operands by transposed reads, two k-steps ahead of their MFMAs
         // (PF & 128: four ahead)
         constexpr int kS = D / 16, kAh = (PF & 128) ? 4 : 2;
         half8 qa8[kAh + 1], oa8[kAh + 1];
         auto rd = [&](int s_) __attribute__((always_inline)) {
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const uint32_t off = q16_off(16 * s_ + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
-            const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
-            if (e == 0) { qa8[s_ % (kAh + 1)].lo = x; oa8[s_ % (kAh + 1)].lo = y; }
-            else { qa8[s_ % (kAh + 1)].hi = x; oa8[s_ % (kAh + 1)].hi = y; }
-          }
+          read_ops(base, s_, qa8[s_ % (kAh + 1)], oa8[s_ % (kAh + 1)]);
         };
+        if constexpr (AHD) {  // read before the barrier (end of the previous step)
+          sacc = nsacc;
+          pacc = npacc;
 #pragma unroll
-        for (int s_ = 0; s_ < kAh; ++s_) rd(s_);
+          for (int s_ = 0; s_ < 2; ++s_) { qa8[s_] = nq8[s_]; oa8[s_] = no8[s_]; }
+        } else {
+          read_rowc(base, sacc, pacc);
+#pragma unroll
+          for (int s_ = 0; s_ < kAh; ++s_) rd(s_);
+        }
         if constexpr ((PF & 1) != 0) __builtin_amdgcn_s_setprio(1);  // the S / dP MFMAs first; the consumer's fill in
 #pragma unroll
         for (int s_ = 0; s_ < kS; ++s_) {
@@ -809,11 +852,16 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       }
       stamp(2);
     };
+    auto pstep2 = [&](auto C_, int it) __attribute__((always_inline)) {
+      constexpr int c = decltype(C_)::value;
+      pstep(C_, it);
+      preread((c + 1) % 4, it + 1);  // (AHD: tile it+1 was stored in step it-1, published by this step's barrier)
+    };
     for (int it = 0; it < nsteps; it += 4) {
-      pstep(IC<0>{}, it);
-      pstep(IC<1>{}, it + 1);
-      pstep(IC<2>{}, it + 2);
-      pstep(IC<3>{}, it + 3);
+      pstep2(IC<0>{}, it);
+      pstep2(IC<1>{}, it + 1);
+      pstep2(IC<2>{}, it + 2);
+      pstep2(IC<3>{}, it + 3);
     }
     stamp_out();
     return;
@@ -1799,6 +1847,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
       case 1412: e = launch_dkdv_pc<128, 64 | 1>(a, s); break;
       case 1413: e = launch_dkdv_pc<128, 128>(a, s); break;  // producer operand reads four k-steps ahead
       case 1420: e = launch_dkdv_pc<128, 256>(a, s); break;  // the edge mask if-converted (before)
+      case 1430: e = launch_dkdv_pc<128, 512>(a, s); break;  // tiles stored two ahead, producer pre-reads
       case 1421: e = launch_dkdv_pc<128, 256>(a, s); break;  // (with 1608's dQ pass)
       case 1414: e = launch_dkdv_pc<128, 128 | 4>(a, s); break;
       case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
