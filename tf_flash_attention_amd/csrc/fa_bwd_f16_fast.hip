@@ -1653,9 +1653,8 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) kb2[s] = k2_off(r, 2 * s + h);
 
-  auto cstep = [&](auto C_, int it) __attribute__((always_inline)) {
+  auto cwork = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;
-    if constexpr (CDP) __syncthreads(); else stage(C_, it);
     const int ka = kt0 + (it - 1) * kBN;
     const int cls = (it >= 1 && it - 1 < ntiles) ? tcls(ka) : 0;
     if (cls == 0) return;
@@ -1685,6 +1684,16 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
       if (n + 2 < kN) rka(n + 2);
       const int s = n / (D / 32), u = n % (D / 32);
       dq[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka8p[n % 3], dsf[s], dq[u], 0, 0, 0);
+    }
+  };
+  // PF & 16 (SLATE): the consumer's dQ MFMAs right after the barrier, its staging after them
+  auto cstep = [&](auto C_, int it) __attribute__((always_inline)) {
+    constexpr int c = decltype(C_)::value;
+    if constexpr (CDP || (PF & 16) != 0) __syncthreads(); else stage(C_, it);
+    cwork(C_, it);
+    if constexpr (!CDP && (PF & 16) != 0) {
+      store_tile((c + 1) % 4, (c + 1) % 2);
+      load_tile(kt0 + kBN * (it + 3), (c + 1) % 2);
     }
   };
   for (int it = 0; it < nsteps; it += 4) {
@@ -1873,6 +1882,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
     if (v == 1601) return launch_dq_pc<128, 1>(a, s);  // ... the producer's MFMAs at priority 1
     if (v == 1604) return launch_dq_pc<128, 4>(a, s);  // ... dPᵀ / dSᵀ formed by the consumer
     if (v == 1608) return launch_dq_pc<128, 8>(a, s);  // ... the edge mask if-converted (before)
+    if (v == 1616) return launch_dq_pc<128, 16>(a, s);  // ... the consumer's staging after its MFMAs
     if (v == 1421) return launch_dq_pc<128, 8>(a, s);
     if (bwd_aligned(a)) return launch_dq_pc<128>(a, s);
     return launch_dq<128, 4, 1, true>(a, s);
