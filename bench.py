@@ -67,17 +67,37 @@ def _call_backward(cfg, q, k, v, o, l, m, do):
     return fa.attention_backward(policy, seq_dims, q, k, v, o, l, m, do, sync, ws, ls, causal)
 
 
+def usable_cpus() -> tuple:
+    """(cpus this process may run on, why): the affinity mask, capped by a cgroup CPU quota when
+    one is set (a GPU box grants each GPU a share of a larger host; os.cpu_count() is the host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    why = "affinity mask"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) // int(period)))
+            if q < n:
+                n, why = q, f"cgroup cpu.max quota ({quota}/{period})"
+    except (OSError, ValueError):
+        pass
+    return n, why
+
+
 def cpu_baseline(cfg, budget_s: float):
     """The reference's naive (TF) CPU attention, restated in numpy fp32
-    (oracle.naive_attention_slice_f32, tests/test_1d.py:69-76), timed on a bounded
-    sample of (b,h) slices of the same workload; fp16 inputs upcast to fp32."""
+    (oracle.naive_attention_slice_f32, tests/test_1d.py:69-76; for a forward+backward config also
+    oracle.naive_attention_backward_slice_f32, the autodiff of that graph), timed on a bounded
+    sample of (b,h) slices of the same workload on every CPU this process may use; fp16 inputs
+    upcast to fp32."""
     from oracle import fa_oracle as O
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])  # BLAS threads actually used
-    except Exception:  # pragma: no cover
-        cores = 1
     policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, _ = cfg
+    ncpu, why = usable_cpus()
+    try:
+        from threadpoolctl import threadpool_info, threadpool_limits
+        limiter = threadpool_limits(limits=ncpu)
+    except Exception:  # pragma: no cover
+        threadpool_info, limiter = None, None
     rng = np.random.default_rng(0)
     nq, nk = int(np.prod(qs)), int(np.prod(ks))
     prob = O.Problem(policy, seq_dims, sync, ws, ls, causal)
@@ -85,23 +105,34 @@ def cpu_baseline(cfg, budget_s: float):
     if policy != "full":
         mask = O.problem_mask(prob, list(qs), list(ks))
     pairs = nq * nk if mask is None else int(mask.sum())
-    flops_slice = 2.0 * (d + d) * pairs
+    flops_slice = 2.0 * (d + d) * pairs + (2.0 * (3 * d + 2 * d) * pairs if bwd else 0.0)
     q = rng.uniform(-2, 2, (d, nq)).astype(np.float32)
     k = rng.uniform(-2, 2, (d, nk)).astype(np.float32)
     v = rng.uniform(-2, 2, (d, nk)).astype(np.float32)
+    do = rng.uniform(-2, 2, (d, nq)).astype(np.float32) if bwd else None
     O.naive_attention_slice_f32(q[:, :64], k[:, :64], v[:, :64])  # warm BLAS threads
+    cores = ncpu
+    if threadpool_info is not None:
+        used = [p.get("num_threads", 1) for p in threadpool_info() if p.get("user_api") == "blas"]
+        cores = max(used or [ncpu])
     n, t0 = 0, time.perf_counter()
     while True:
         O.naive_attention_slice_f32(q, k, v, mask)
+        if bwd:
+            O.naive_attention_backward_slice_f32(q, k, v, do, mask)
         n += 1
         el = time.perf_counter() - t0
         if el >= budget_s or n >= int(np.prod(batch)):
             break
+    if limiter is not None:
+        limiter.restore_original_limits()
     tflops = flops_slice * n / el / 1e12
+    what = "forward + backward" if bwd else "forward"
     return {"value": tflops, "unit": "TFLOP/s", "cores": int(cores), "kind": "port",
-            "host_cpus": os.cpu_count(), "cpu_model": _cpu_model(),
-            "sample": f"{n} of {int(np.prod(batch))} (b,h) slices of the workload, numpy fp32 naive attention "
-                      f"(einsum->softmax->einsum, tests/test_1d.py:69-76), {el:.1f}s; fp16 inputs upcast"}
+            "host_cpus": os.cpu_count(), "usable_cpus": ncpu, "usable_cpus_from": why, "cpu_model": _cpu_model(),
+            "sample": f"{n} of {int(np.prod(batch))} (b,h) slices of the workload, {what}, numpy fp32 naive attention "
+                      f"(einsum->softmax->einsum, tests/test_1d.py:69-76; backward = its autodiff) on "
+                      f"{cores} BLAS threads, {el:.1f}s; fp16 inputs upcast"}
 
 
 def _cpu_model() -> str:
@@ -130,9 +161,25 @@ def spawn_ranks(n: int, argv) -> int:
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
-    codes = [p.wait() for p in procs]
-    bad = [c for c in codes if c != 0]
-    return bad[0] if bad else 0
+    # poll: the first rank that fails ends the others (they would otherwise wait in the gloo
+    # rendezvous or barrier for its 30-minute timeout), and its status is returned
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad[0]
+        if all(c == 0 for c in codes):
+            return 0
+        time.sleep(0.05)
 
 
 def algorithmic_bytes(cfg, b):
@@ -191,7 +238,8 @@ def main():
         devnull = os.open(os.devnull, os.O_WRONLY)
         os.dup2(devnull, 1)
         try:
-            dist.init_process_group("gloo")
+            import datetime
+            dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=5))
         finally:
             os.dup2(saved, 1)
             os.close(devnull)

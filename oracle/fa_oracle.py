@@ -422,3 +422,52 @@ def naive_attention_slice_f32(q: np.ndarray, k: np.ndarray, v: np.ndarray, mask=
     if mask is not None:
         p = np.where(mask, p, np.float32(0))
     return v @ p.T
+
+
+def naive_attention_backward_slice_f32(q, k, v, do, mask=None):
+    """The gradients TF's autodiff takes through the naive graph of tests/test_1d.py:69-76
+    (einsum -> where -> softmax -> where -> einsum), restated in numpy float32 for one slice:
+    the CPU leg of a forward+backward step.  Recomputes P like the graph's saved activations
+    would hold it.  q [d, nq], k [d, nk], v [vd, nk], do [vd, nq] -> (dq, dk, dv)."""
+    d = q.shape[0]
+    sc = np.float32(1.0 / math.sqrt(d))
+    logit = (q.T @ k) * sc
+    if mask is not None:
+        logit = np.where(mask, logit, np.finfo(np.float32).min)
+    logit -= logit.max(axis=1, keepdims=True)
+    p = np.exp(logit)
+    p /= p.sum(axis=1, keepdims=True)
+    if mask is not None:
+        p = np.where(mask, p, np.float32(0))
+    dv = do @ p                                   # [vd, nk]
+    dp = do.T @ v                                 # [nq, nk]
+    ds = p * (dp - np.sum(dp * p, axis=1, keepdims=True)) * sc
+    return k @ ds.T, q @ ds, dv
+
+
+def forward_rows_f64(q, k, v, prob: Problem, q_seq, k_seq, r0: int, r1: int, k0: int = 0, k1=None):
+    """Float64 forward of query rows [r0, r1) of ONE slice (q [d, nq], k [d, nk], v [vd, nk]):
+    the same math as :func:`forward_f64`, for sequences too long to walk whole.  The rule is
+    evaluated for those rows against keys [k0, k1) (default: every key); a caller narrows the
+    range only where the rule provably allows nothing outside it (a 1d window around the rows).
+    Returns (O [vd, r1-r0], L, M, has_any)."""
+    ev = _evaluator(prob, q_seq, k_seq)
+    d = q.shape[0]
+    scale = 1.0 / math.sqrt(d)
+    k1 = k.shape[1] if k1 is None else k1
+    mk_full = np.zeros((r1 - r0, k.shape[1]), dtype=bool)
+    mk_full[:, k0:k1] = ev.block(r0, r1, k0, k1)
+    cols = np.nonzero(mk_full.any(axis=0))[0]
+    ha = mk_full.any(axis=1)
+    vd = v.shape[0]
+    if cols.size == 0:
+        return np.zeros((vd, r1 - r0)), np.zeros(r1 - r0), np.zeros(r1 - r0), ha
+    c0, c1 = int(cols[0]), int(cols[-1]) + 1
+    mk = mk_full[:, c0:c1]
+    s = np.where(mk, (q[:, r0:r1].astype(np.float64).T @ k[:, c0:c1].astype(np.float64)) * scale, -np.inf)
+    mrow = np.where(ha, s.max(axis=1), 0.0)
+    p = np.exp(s - mrow[:, None])
+    lrow = p.sum(axis=1)
+    o = v[:, c0:c1].astype(np.float64) @ (p / np.where(ha, lrow, 1.0)[:, None]).T
+    o[:, ~ha] = 0.0
+    return o, np.where(ha, lrow, 0.0), mrow, ha

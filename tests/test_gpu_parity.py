@@ -396,7 +396,7 @@ def diag_lib(monkeypatch):
         pytest.skip("libfa_hip_diag.so not built (make -C tf_flash_attention_amd diag)")
     with _lib.using(_lib.DIAG_LIB_PATH):
         info = _lib.build_info()
-        assert "lib=diag" in info and f"src={_lib.source_hash()};" in info, info
+        assert "lib=diag" in info and f"src={_lib.source_hash(diag=True)};" in info, info
         yield
 
 

@@ -180,3 +180,32 @@ def test_flop_counts():
     assert O.allowed_pairs(O.Problem("causal", 1), [100], [100]) == 100 * 101 // 2
     n, ws = 300, 16
     assert O.allowed_pairs(O.Problem("local", 1, "none_front", ws), [n], [n]) == n * (2 * ws - 1) - ws * (ws - 1)
+
+
+def test_naive_backward_matches_f64_backward():
+    """The CPU baseline's fp32 naive backward (the autodiff of tests/test_1d.py:69-76) agrees with
+    the float64 oracle's analytic gradients."""
+    rng = np.random.default_rng(11)
+    d, nq, nk = 16, 70, 90
+    q, k, v, do = (rng.uniform(-2, 2, s).astype(np.float32) for s in ((d, nq), (d, nk), (d, nk), (d, nq)))
+    prob = O.Problem("causal", 1, "scale_end")
+    mask = O.problem_mask(prob, [nq], [nk])
+    dq, dk, dv = O.naive_attention_backward_slice_f32(q, k, v, do, mask)
+    rq, rk, rv = O.backward_f64(q[None], k[None], v[None], do[None], prob)
+    for got, ref in ((dq, rq[0]), (dk, rk[0]), (dv, rv[0])):
+        np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+
+
+def test_forward_rows_matches_forward():
+    """forward_rows_f64 (row ranges of one long slice) equals forward_f64 on those rows."""
+    rng = np.random.default_rng(12)
+    d, nq, nk = 8, 300, 260
+    q, k, v = (rng.uniform(-2, 2, s) for s in ((d, nq), (d, nk), (d, nk)))
+    prob = O.Problem("local", 1, "scale_front", 37, 0, True)
+    Of, Lf, Mf, haf = O.forward_f64(q[None], k[None], v[None], prob)
+    for r0, r1 in ((0, 5), (100, 180), (290, 300)):
+        o, l, m, ha = O.forward_rows_f64(q, k, v, prob, [nq], [nk], r0, r1)
+        np.testing.assert_allclose(o, Of[0][:, r0:r1], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(l, Lf[0][r0:r1], rtol=1e-12)
+        np.testing.assert_allclose(m, Mf[0][r0:r1], rtol=1e-12)
+        assert (ha == haf[r0:r1]).all()

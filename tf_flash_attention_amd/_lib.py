@@ -64,7 +64,7 @@ class FaProblem(ctypes.Structure):
 
 _lock = threading.Lock()
 _lib = None
-_override = None  # a library routed in by using() (tests: the diagnostic build's variants)
+_tls = threading.local()  # .override: a library routed in by using() on THIS thread (tests: the diag build)
 _loaded = {}
 DIAG_LIB_PATH = os.path.join(_HERE, "libfa_hip_diag.so")
 
@@ -103,8 +103,9 @@ def _declare(lib):
 def lib():
     """Load (once) and return the HIP library, or raise LibraryNotBuiltError."""
     global _lib
-    if _override is not None:
-        return _override
+    ov = getattr(_tls, "override", None)
+    if ov is not None:
+        return ov
     if _lib is not None:
         return _lib
     with _lock:
@@ -126,19 +127,20 @@ def using(path):
 
     The GPU tests use it to run the diagnostic build (libfa_hip_diag.so, ``make -C
     tf_flash_attention_amd diag``): its FA_FWD_VARIANT / FA_BWD_VARIANT structures are not in
-    the product library.  ctypes loads each library RTLD_LOCAL, so both can live in one process."""
-    global _override
+    the product library.  ctypes loads each library RTLD_LOCAL, so both can live in one process.
+    The routing is per thread: calls from other threads keep the product library."""
     with _lock:
         h = _loaded.get(path)
         if h is None:
             if not os.path.exists(path):
                 raise LibraryNotBuiltError(f"library not found at {path}")
             h = _loaded[path] = _declare(ctypes.CDLL(path))
-    prev, _override = _override, h
+    prev = getattr(_tls, "override", None)
+    _tls.override = h
     try:
         yield h
     finally:
-        _override = prev
+        _tls.override = prev
 
 
 def make_problem(dtype, policy, seq_dims, sync_mode, b, q_seq, k_seq, d, v_d,
@@ -154,13 +156,16 @@ def make_problem(dtype, policy, seq_dims, sync_mode, b, q_seq, k_seq, d, v_d,
     return p
 
 
-def source_hash() -> str:
+def source_hash(diag: bool = False) -> str:
     """sha256 (first 16 hex digits) of the product sources, computed exactly as the Makefile's
-    SRC_HASH (csrc/*.hip, csrc/*.h, ../include/fa_api.h in make's byte-wise sort order)."""
+    SRC_HASH (csrc/*.hip, csrc/*.h, ../include/fa_api.h in make's byte-wise sort order); with
+    ``diag`` the diagnostic library's DIAG_HASH, which also covers csrc/diag/*.hip."""
     import glob
     import hashlib
-    rel = [os.path.relpath(p, _HERE) for p in glob.glob(os.path.join(_HERE, "csrc", "*.hip"))
-           + glob.glob(os.path.join(_HERE, "csrc", "*.h"))] + ["../include/fa_api.h"]
+    files = glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.h"))
+    if diag:
+        files += glob.glob(os.path.join(_HERE, "csrc", "diag", "*.hip"))
+    rel = [os.path.relpath(p, _HERE) for p in files] + ["../include/fa_api.h"]
     h = hashlib.sha256()
     for r in sorted(rel, key=lambda x: x.encode()):
         with open(os.path.join(_HERE, r), "rb") as f:

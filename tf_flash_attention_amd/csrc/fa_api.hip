@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
@@ -51,6 +52,27 @@ hipError_t set_smem_once(const void* kern, int bytes) {
   e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
   if (e == hipSuccess) done.push_back({kern, dev, bytes});
   return e;
+}
+
+int device_cus() {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev];  // 0 = not queried yet (a benign race: same value)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  if (dev >= 0 && dev < kMaxDev) {
+    const int c = cache[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
+  }
+  int cus = 0;
+  if (dev < 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  if (dev >= 0 && dev < kMaxDev) cache[dev].store(cus, std::memory_order_relaxed);
+  return cus;
+}
+
+int device_xcds() {
+  const int x = device_cus() / 32;
+  return x < 1 ? 1 : (x > 8 ? 8 : x);
 }
 
 }  // namespace fa

@@ -58,6 +58,14 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
 // (fa_api.hip); later launches of the same kernel on the same device skip the runtime call
 hipError_t set_smem_once(const void* kern, int bytes);
 
+// host: compute units of the current device, cached per device id (fa_api.hip; thread-safe).
+// Persistent grids size themselves from it.
+int device_cus();
+// host: XCDs of the current device as the CU count implies (32 CUs per gfx950 XCD; a compute
+// partition exposes fewer), at least 1, at most 8.  Speed only: the XCD-aware block orders
+// assume round-robin dispatch over this many XCDs.
+int device_xcds();
+
 #ifdef FA_DIAG
 // host, diagnostic library only (libfa_hip_diag.so, built with -DFA_DIAG for tools/): A/B and
 // ablation variants are selected from the environment.  The product library has no variant code

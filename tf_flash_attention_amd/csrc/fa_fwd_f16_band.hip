@@ -72,6 +72,7 @@ struct BandArgs {
   int32_t T;        // tile positions per item
   int32_t n_wg;     // workgroups (persistent)
   int32_t inter;    // 1: XCD-interleaved item order (below)
+  int32_t n_xcd;    // XCDs the workgroups are dealt over (device_xcds(); n_wg % n_xcd == 0 when inter)
 };
 
 template <int B, int E, typename F>
@@ -105,18 +106,18 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   const int nqb = (nq + kBM - 1) / kBM;
   // this workgroup's items: first + stride * local, inside [it_begin, it_end).
   //   contiguous: a run of consecutive items per workgroup (stride 1);
-  //   XCD-interleaved (inter): the eight XCDs (workgroup g runs on XCD g mod 8) each take one eighth
-  //   of the items, and the J workgroups of an XCD take every J-th item of it, so at any time an
+  //   XCD-interleaved (inter): the X XCDs (workgroup g runs on XCD g mod X; X = 8 on a whole MI355X)
+  //   each take one X-th of the items, and the J workgroups of an XCD take every J-th item of it, so at any time an
   //   XCD's CUs walk J consecutive items whose key bands overlap: each K/V tile is re-read from that
   //   XCD's L2 instead of re-fetched (a contiguous run re-reads a tile one and two items later, a
   //   window of ~24 tiles per CU that the 4 MB L2 shared by 32 CUs does not hold)
   const int64_t g = blockIdx.x;
   int64_t it_begin, it_end, first, stride;
   if (ba.inter) {
-    const int64_t x = g & 7, J = (ba.n_wg - x + 7) >> 3;
-    it_begin = x * ba.n_items / 8;
-    it_end = (x + 1) * ba.n_items / 8;
-    first = it_begin + (g >> 3);
+    const int64_t X = ba.n_xcd, x = g % X, J = (ba.n_wg - x + X - 1) / X;
+    it_begin = x * ba.n_items / X;
+    it_end = (x + 1) * ba.n_items / X;
+    first = it_begin + g / X;
     stride = J;
   } else {
     it_begin = g * ba.n_items / ba.n_wg;
@@ -584,21 +585,13 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   if (grp == 0) __builtin_amdgcn_s_barrier();
 }
 
-int g_cus = 0;
-
 int64_t band_workgroups(int64_t n_items) {
-  if (g_cus == 0) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    g_cus = cus;
-  }
-  return n_items < g_cus ? n_items : g_cus;
+  const int cus = device_cus();  // per device (fa_api.hip)
+  return n_items < cus ? n_items : cus;
 }
 
 // the XCD-interleaved item order needs whole XCD groups and several items per workgroup
-bool band_interleaved(int64_t n_items, int64_t n_wg) { return n_wg % 8 == 0 && n_items >= 2 * n_wg; }
+bool band_interleaved(int64_t n_items, int64_t n_wg, int n_xcd) { return n_wg % n_xcd == 0 && n_items >= 2 * n_wg; }
 
 struct TCache {
   Rule r;
@@ -641,9 +634,13 @@ bool fwd_f16_band_supported(const FwdArgs& a) {
     return false;
   // a band: every block spans few tiles (else the per-launch kernels cover it at no loss)
   if (band_tiles_per_item(a) > 24) return false;
+  // the per-slice table of first key tiles lives in LDS: kMaxTab query blocks (nq <= 1M)
+  if ((nq + kBM - 1) / kBM > kMaxTab) return false;
   // one descriptor per tensor spans a workgroup's slices: below 2^31 bytes
   const int64_t nqb = (nq + kBM - 1) / kBM, n_items = a.b * nqb, n_wg = band_workgroups(n_items);
-  const int64_t span = (band_interleaved(n_items, n_wg) ? (n_items + 7) / 8 : (n_items + n_wg - 1) / n_wg) / nqb + 2;
+  const int xcds = device_xcds();
+  const int64_t span =
+      (band_interleaved(n_items, n_wg, xcds) ? (n_items + xcds - 1) / xcds : (n_items + n_wg - 1) / n_wg) / nqb + 2;
   return span * 2 * (int64_t)dm * (nq > nk ? nq : nk) < (1ll << 31);
 }
 
@@ -661,7 +658,8 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   ba.T = band_tiles_per_item(a);
   ba.n_items = a.b * (int64_t)((a.rule.q.n + kBM - 1) / kBM);
   ba.n_wg = (int)band_workgroups(ba.n_items);
-  ba.inter = band_interleaved(ba.n_items, ba.n_wg) ? 1 : 0;
+  ba.n_xcd = device_xcds();
+  ba.inter = band_interleaved(ba.n_items, ba.n_wg, ba.n_xcd) ? 1 : 0;
 #ifdef FA_DIAG
   const int dv = diag_variant("FA_FWD_VARIANT");
   if (dv == 2401 && ba.T == 12) return launch_band_t<12, true>(ba, s);
