@@ -527,6 +527,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         __builtin_amdgcn_sched_barrier(0);  // the epilogue's temporaries die before the softmax's
         m_max = kNegInf;
         thr = -__FLT_MAX__;  // the item's first allowed key seeds m_run (scores are relative to it)
+        m_run = 0.f;         // (this item's first Sᵀ ran against -m = 0: see the end of VALU(T-1))
         item_state(cur);
       }
     }
@@ -543,7 +544,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         for (int y = 0; y < 4; ++y) lacc[y] = 0.f;
       }
     }
-    if constexpr (it == T - 1) read_q((n + 1) & 1);  // before this wave's first Sᵀ of the next item
+    if constexpr (it == T - 1) {
+      read_q((n + 1) & 1);  // before this wave's first Sᵀ of the next item
+      // the next item's scores start relative to 0, not to this item's m_run: an item's result
+      // must not depend on the item the workgroup walked before it (bitwise: a slice's O / l / m
+      // are the same wherever it sits in the batch)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) negm[i] = 0.f;
+    }
   };
 
   const int grp = w >> 2;  // waves w and w+4 share a SIMD
