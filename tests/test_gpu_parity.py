@@ -296,6 +296,16 @@ def test_odd_channels(d, vd):
         run_case(dt, "causal", 1, "scale_front", (1, 2), d, vd, (150,), (75,), seed=d)
 
 
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
+@pytest.mark.parametrize("d,vd", [(160, 160), (256, 256), (130, 300), (520, 72), (300, 1030)])
+@pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, True)])
+def test_wide_channels(dtype, d, vd, policy, ws, causal):
+    """Channel counts past the MFMA kernels' 128: the resident generic kernels up to 256 (fp16 /
+    fp32) / 128 (fp64) channels, the channel-chunked kernels past that (the reference has no fixed
+    channel cap either: its key tile is sized from shared memory, flash_attention.cu:1977-2067)."""
+    run_case(dtype, policy, 1, "scale_front", (2,), d, vd, (97,), (150,), ws=ws, causal=causal, seed=d + vd)
+
+
 # --------------------------------------------------------------- edge cases
 @pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
 @pytest.mark.parametrize("nq,nk", [(1, 1), (1, 77), (77, 1), (2, 3), (64, 64), (65, 63)])
