@@ -15,8 +15,8 @@
 //   * the K/V staging (registers, loads five / four positions ahead, stored two positions
 //     later; LDS rings of four slots) runs straight across item boundaries;
 //   * the next item's Q image is loaded one 16-B chunk per thread at positions 2-5 and stored
-//     into the second of two LDS Q buffers at 4-7; each wave reads its new Q fragments in the
-//     VALU phase of the item's last position;
+//     into the second of two LDS Q buffers one position later (3-6); each wave reads its new Q
+//     fragments in the VALU phase of the item's last position;
 //   * at position 0 of the next item the waves write the finished item's O (fp16, [c][256 q])
 //     over its dead Q buffer and its l / m beside it; at positions 2-3 whole 16-B rows leave
 //     for HBM (coalesced; the per-value stores of a per-block kernel touch 32-64 lines each);
@@ -61,10 +61,24 @@ constexpr int kMaxTab = 4096;                 // query blocks per slice: nq <= 1
 constexpr int kSmem = kOffTab + 4 * kMaxTab;  // 145.5 KB
 // Item timeline (positions it = 0 .. T-1 of item n+1): VALU(0) writes item n's O / l / m into
 // LDS (O over Q buffer n&1, dead by then); MFMA(2), MFMA(3) store it to HBM; MFMA(2..5) load
-// item n+2's Q chunks, MFMA(4..7) store them into buffer n&1 (after the O reads); VALU(T-1)
+// item n+2's Q chunks, MFMA(3..6) store them into buffer n&1 (after the O reads); VALU(T-1)
 // reads them as fragments: with T >= 12 a barrier separates every store from every read.
 constexpr int kMinT = 12;
+// structure flags: the rebase check and m on the packed P (fa_fwd_f16_pingpong.hip's kFPMax; the
+// default since round 3; 0 = round 2's exact fp32 row max on every tile)
+constexpr int kBFPMax = 1;
+constexpr int kBandDefault = kBFPMax;
+// timing ablations (diagnostic library only; outputs WRONG): no edge masks, no item-boundary traffic
+// (O / l / m out, next Q in), no softmax (P = S rounded)
+constexpr int kBANoMask = 2, kBANoItem = 4, kBANoSoftmax = 8;
+// ... every staging load re-reading one hot tile (L2-resident), no staging LDS stores
+constexpr int kBANoLoad = 16, kBANoStore = 32;
+// ... parts of the item-boundary traffic: O / l / m into LDS, their HBM stores, the next Q
+constexpr int kBANoEpi = 64, kBANoOStore = 128, kBANoQ = 256;
 constexpr float kRescaleThr = 8.f;
+// masked scores sit at or below -2^19 (the arithmetic edge mask); a row maximum at or below this
+// floor means "nothing allowed yet" (never a reference), and is the unset state of thr
+constexpr float kMaskFloor = -262144.f;
 
 struct BandArgs {
   FwdArgs a;
@@ -94,8 +108,9 @@ struct Item {
 // its positions, so ring slots, staging sets and every "which position of the item" decision are
 // compile-time (no per-phase selects or dummy operations) and a position p = n*T + it has
 // p mod 4 == it mod 4
-template <int T, bool STAMP = false>
+template <int T, bool STAMP = false, int F = kBandDefault>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) {
+  constexpr bool PMAX = (F & kBFPMax) != 0;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
   const FwdArgs& a = ba.a;
@@ -152,17 +167,33 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     *reinterpret_cast<__attribute__((address_space(3))) int*>(smem + kOffTab + 4 * qb) = (kb / kBN) * kBN;
   }
   __syncthreads();
+  // the walk's item index n = first + local * stride as (slice, query block), advanced by
+  // scalar adds (the host keeps n_items below 2^31; a 64-bit division per item lowered to ~100
+  // scalar and vector instructions and spilled SGPRs across the stream)
+  int walk_sl = 0, walk_qb = 0;
+  {
+    const int n0 = (int)((first < it_end ? first : it_begin) - sl0 * nqb);  // (relative to sl0)
+    walk_sl = __builtin_amdgcn_readfirstlane(n0 / nqb);
+    walk_qb = __builtin_amdgcn_readfirstlane(n0 - walk_sl * nqb);
+  }
+  const int stride_qb = __builtin_amdgcn_readfirstlane((int)(stride % nqb)),
+            stride_sl = __builtin_amdgcn_readfirstlane((int)(stride / nqb));
+  // the item at the walk position, then the walk advanced by one stride
   auto make_item = [&](int local) -> Item {
     Item x;
     const bool live = local < n_local;
-    const int64_t n = live ? first + (int64_t)local * stride : it_begin;
-    // (64-bit division lowers to VALU code: readfirstlane keeps the results in SGPRs, else every
-    // buffer op that takes them in soffset becomes a waterfall loop)
-    x.sl = __builtin_amdgcn_readfirstlane((int)(n / nqb - sl0));
-    const int qb = __builtin_amdgcn_readfirstlane((int)(n % nqb));
-    x.q0 = live ? qb * kBM : nq;
-    const int kt0 = *reinterpret_cast<const __attribute__((address_space(3))) int*>(tab + 4 * qb);
+    x.sl = live ? walk_sl : 0;  // (a dead item reads zeros from slice 0: offsets stay in range)
+    x.q0 = live ? walk_qb * kBM : nq;
+    const int kt0 = *reinterpret_cast<const __attribute__((address_space(3))) int*>(tab + 4 * walk_qb);
     x.kt0 = live ? __builtin_amdgcn_readfirstlane(kt0) : nk;
+    if (live) {
+      walk_qb += stride_qb;
+      walk_sl += stride_sl;
+      if (walk_qb >= nqb) {
+        walk_qb -= nqb;
+        ++walk_sl;
+      }
+    }
     return x;
   };
   Item cur = make_item(0), nxt = make_item(1);
@@ -184,12 +215,16 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   const int qc0 = tid >> 5, qm = tid & 31;
   const uint32_t qg_lane = (uint32_t)qc0 * (uint32_t)nq * 2u + 16u * qm;
   const uint32_t ql_lane = qc0 * kQRow + ((qm * 16) ^ ((qc0 & 3) << 6));
-  // (inside the item loop the lane offsets are made opaque where used: hoisted per chunk they
-  // would stay live across the whole stream)
+  // (inside the item loop the lane offsets are recomputed where used from an opaque copy of the
+  // thread id: hoisted, they would stay live across the whole stream, a VGPR each)
+  auto opaque_tid = [&]() -> int __attribute__((always_inline)) {
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    return t;
+  };
   auto qload = [&](const Item& x, int j) -> u32x4 __attribute__((always_inline)) {
-    uint32_t qg = qg_lane;
-    int qc = qc0, qq = 8 * qm;
-    asm volatile("" : "+v"(qg), "+v"(qc), "+v"(qq));
+    const int t = opaque_tid(), qc = t >> 5, qq = 8 * (t & 31);
+    const uint32_t qg = (uint32_t)qc * (uint32_t)nq * 2u + 2u * (uint32_t)qq;
     const bool in = qc + 16 * j < d && x.q0 + qq < nq;
     return __builtin_amdgcn_raw_buffer_load_b128(qrs, in ? qg + (uint32_t)j * 32u * (uint32_t)nq : 0x80000000u,
                                                  x.sl * qsl + 2 * min(x.q0, nq), 0);
@@ -257,7 +292,12 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         klo = min(max(qo - (R.ws - 1) - R.k.o0, 0), nk);
         khi = min(ohi - R.k.o0, nk - 1);
       } else {
-        key_interval(R, min(qi, nq - 1), &klo, &khi);
+        // (strides made opaque here: else hipcc hoists the divisions' reciprocals to the kernel
+        // top, and they stay live, spilled, across the whole stream)
+        Rule R2 = R;
+        R2.seq_dims = 1;  // (the host admits 1d rules only: no 2d coordinate division compiled in)
+        asm volatile("" : "+s"(R2.k.s0), "+s"(R2.q.s0));
+        key_interval(R2, min(qi, nq - 1), &klo, &khi);
       }
       kspan = max(khi - klo + 1, 0);
       const int last = min(31, nq - 1 - wq0);
@@ -268,11 +308,15 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     }
   };
   item_state(cur);
-  // tile class of position `it` of the current item: 0 no allowed pair, 1 mixed, 2 all allowed
+  // tile class of position `it` of the current item: 0 no allowed pair, 2 all allowed; mixed: 3 only
+  // some lanes' first allowed key lies inside the tile (the band's leading edge), 4 only some lanes'
+  // last one (the trailing edge), 1 both (windows narrower than a tile).  (khi <= nk - 1 for every
+  // lane, so the tail past nk is a trailing edge.)
   auto tcls = [&](int it) -> int __attribute__((always_inline)) {
     const int k0 = cur.kt0 + it * kBN, k1 = k0 + kBN - 1;
     if (!wave_active || wlo_min > k1 || whi_max < k0) return 0;
-    return (wlo_max <= k0 && whi_min >= k1 && k1 < nk) ? 2 : 1;
+    const bool lo = wlo_max > k0, hi = whi_min < k1;
+    return lo ? (hi ? 1 : 3) : (hi ? 4 : 2);
   };
 
   // fragment read bases (lane constants), as fa_fwd_f16_pingpong.hip
@@ -311,18 +355,32 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     o[1][i] = 0.f;
     negm[i] = 0.f;
   }
-  float m_run = 0.f, m_max = kNegInf, thr = -__FLT_MAX__;
+  float m_run = 0.f, m_max = kNegInf, thr = kMaskFloor;
   float lacc[4] = {0.f, 0.f, 0.f, 0.f};
 
-  auto mask = [&](int k0) __attribute__((always_inline)) {
-    const int base = k0 + 8 * h - klo;  // allowed iff base + o in [0, kspan)
+  // edge-tile mask, arithmetic: key k0 + 8h + off is allowed iff 0 <= base + off < kspan (base = k0 +
+  // 8h - klo), so min(s, (base + off + 0.5)·2^20) (leading edge) and min(s, (kspan - base - off -
+  // 0.5)·2^20) (trailing edge) keep an allowed score (the bound is >= 2^19) and take a disallowed one
+  // to <= -2^19, whose exp2 is 0 against any reference.  One fma and one min per score and edge, no
+  // compare, no VCC select and so no hazard wait (the select form cost an add, a compare, a 2-state
+  // s_nop and a v_cndmask per score); one copy of the code serves both edges (the edge picks the
+  // per-lane constant and the sign), and a tile holding both edges (windows narrower than a tile)
+  // runs it twice.  Rows with nothing allowed stay below kMaskFloor (never seeded).
+  auto mask = [&](int k0, int cls) __attribute__((always_inline)) {
+    constexpr float kBig = 1048576.f;
+    const float fb = (float)(k0 + 8 * h - klo);
+    const float ca = __builtin_fmaf(fb, kBig, 0.5f * kBig), cb = __builtin_fmaf((float)kspan - fb, kBig, -0.5f * kBig);
+    const int npass = cls == 1 ? 2 : 1;
+#pragma nounroll
+    for (int pass = 0; pass < npass; ++pass) {
+      const bool lo = (cls == 3) || (cls == 1 && pass == 0);
+      const float cc = lo ? ca : cb, sg = lo ? kBig : -kBig;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int off = 32 * t + 16 * (i >> 3) + (i & 7);
-        st[t][i] = ((unsigned)(base + off) < (unsigned)kspan) ? st[t][i] : kNegInf;
-      }
+        for (int i = 0; i < 16; ++i)
+          st[t][i] = fminf(st[t][i], __builtin_fmaf(sg, (float)(32 * t + 16 * (i >> 3) + (i & 7)), cc));
+    }
   };
   auto exp_cvt = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -334,8 +392,8 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
                                                        (_Float16)__builtin_amdgcn_exp2f(s1)});
       }
   };
-  auto softmax = [&](int it, int cls, bool first) __attribute__((always_inline)) {
-    if (cls == 1) mask(cur.kt0 + it * kBN);
+  // the exact fp32 row max of the tile (both key halves)
+  auto row_max = [&]() -> float __attribute__((always_inline)) {
     float mx[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) mx[j] = fmaxf(st[j >> 1][8 * (j & 1)], st[j >> 1][8 * (j & 1) + 1]);
@@ -344,13 +402,36 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         mx[j] = fmaxf(fmaxf(mx[j], st[j >> 1][8 * (j & 1) + i]), st[j >> 1][8 * (j & 1) + i + 1]);
-    const float mt = max_pair32(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
-    m_max = fmaxf(m_max, m_run + mt);
+    return max_pair32(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
+  };
+  // PMAX: the running max of P over the current epoch (per lane) and 2^thr (-1: no reference yet)
+  half2v pmr = {(_Float16)0.f, (_Float16)0.f};
+  _Float16 thr_h = (_Float16)-1.f;
+  auto pmax_tile = [&]() -> half2v __attribute__((always_inline)) {
+    auto M3 = [](half2v x, half2v y, half2v z) __attribute__((always_inline)) {
+      return __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z);
+    };
+    auto H = [&](int s_, int x) __attribute__((always_inline)) { return __builtin_bit_cast(half2v, pw[s_][x]); };
+    half2v a0 = M3(H(0, 0), H(0, 1), H(0, 2)), b0 = M3(H(2, 0), H(2, 1), H(2, 2));
+    a0 = M3(a0, H(0, 3), H(1, 0));
+    b0 = M3(b0, H(2, 3), H(3, 0));
+    a0 = M3(a0, H(1, 1), H(1, 2));
+    b0 = M3(b0, H(3, 1), H(3, 2));
+    return M3(M3(a0, H(1, 3), H(3, 3)), b0, b0);
+  };
+  auto softmax = [&](int it, int cls, bool first) __attribute__((always_inline)) {
+    if (cls != 2 && !(F & kBANoMask)) mask(cur.kt0 + it * kBN, cls);
     if (first) {  // an item's first tile: nothing to rescale (O and l start fresh): seed, then exp once
-      const bool seed = mt > -__FLT_MAX__;  // else (an empty row so far) a later tile seeds
+      const float mt = row_max();
+      m_max = fmaxf(m_max, m_run + mt);
+      const bool seed = mt > kMaskFloor;  // else (an empty row so far) a later tile seeds
       const float delta = seed ? mt : 0.f;
       m_run += delta;
-      thr = seed ? kRescaleThr : -__FLT_MAX__;
+      if constexpr (!PMAX) thr = seed ? kRescaleThr : kMaskFloor;
+      if constexpr (PMAX) {
+        thr_h = seed ? (_Float16)(1 << (int)kRescaleThr) : (_Float16)-1.f;
+        pmr = half2v{(_Float16)0.f, (_Float16)0.f};
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         st[0][i] -= delta;
@@ -358,30 +439,68 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         negm[i] = -m_run;
       }
       exp_cvt();
+    } else if constexpr (PMAX) {
+      // the rebase check on the packed P (fa_fwd_f16_pingpong.hip, kFPMax): the exponentials run
+      // against m_run anyway; the exact fp32 max is formed only in the (rare) rebase branch
+      exp_cvt();
+#pragma unroll
+      for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
+        asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
+      const half2v tm = pmax_tile();
+      const _Float16 tmx = __builtin_elementwise_maximum(tm[0], tm[1]);
+      const half2v pmr_old = pmr;
+      pmr = __builtin_elementwise_maximum(pmr, tm);
+      if (__any(tmx > thr_h)) {
+        const float mt = row_max();
+        // close the epoch: its P maximum (approximate) and this tile (exact) into m_max
+        const float pold = (float)__builtin_elementwise_maximum(pmr_old[0], pmr_old[1]);
+        m_max = fmaxf(m_max, fmaxf(m_run + mt, m_run + __log2f(pold)));
+        // (PMAX: thr_h alone carries the state: -1 until the row has a reference)
+        const bool unset = thr_h < (_Float16)0.f;
+        const bool seed = unset && (mt > kMaskFloor);
+        const float delta = unset ? (seed ? mt : 0.f) : fmaxf(mt, 0.f);
+        const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
+        m_run += delta;
+        thr_h = (unset && !seed) ? (_Float16)-1.f : (_Float16)(1 << (int)kRescaleThr);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) lacc[x] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          o[0][i] *= alpha;
+          o[1][i] *= alpha;
+          st[0][i] -= delta;
+          st[1][i] -= delta;
+          negm[i] = -m_run;
+        }
+        exp_cvt();
+        pmr = half2v{(_Float16)0.f, (_Float16)0.f};
+      }
     } else {
-    exp_cvt();
-#pragma unroll
-    for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
-      asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
-    if (__any(mt > thr)) {
-      const bool unset = thr < 0.f;
-      const bool seed = unset && (mt > thr);
-      const float delta = unset ? (seed ? mt : 0.f) : fmaxf(mt, 0.f);
-      const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
-      m_run += delta;
-      thr = (unset && !seed) ? thr : kRescaleThr;
-#pragma unroll
-      for (int x = 0; x < 4; ++x) lacc[x] *= alpha;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        o[0][i] *= alpha;
-        o[1][i] *= alpha;
-        st[0][i] -= delta;
-        st[1][i] -= delta;
-        negm[i] = -m_run;
-      }
+      const float mt = row_max();
+      m_max = fmaxf(m_max, m_run + mt);
       exp_cvt();
-    }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
+        asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
+      if (__any(mt > thr)) {
+        const bool unset = thr < 0.f;
+        const bool seed = unset && (mt > thr);
+        const float delta = unset ? (seed ? mt : 0.f) : fmaxf(mt, 0.f);
+        const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
+        m_run += delta;
+        thr = (unset && !seed) ? thr : kRescaleThr;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) lacc[x] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          o[0][i] *= alpha;
+          o[1][i] *= alpha;
+          st[0][i] -= delta;
+          st[1][i] -= delta;
+          negm[i] = -m_run;
+        }
+        exp_cvt();
+      }
     }
     const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
 #pragma unroll
@@ -399,6 +518,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   auto epilogue_lds = [&]() __attribute__((always_inline)) {
     const float l_tot = sum_pair32((lacc[0] + lacc[1]) + (lacc[2] + lacc[3]));
     const float inv = (l_tot > 0.f) ? __builtin_amdgcn_rcpf(l_tot) : 0.f;
+    // (PMAX: m_max is per lane; the open epoch's P maximum closes it)
+    const float m_fin = PMAX ? max_pair32(fmaxf(m_max, m_run + __log2f((float)__builtin_elementwise_maximum(pmr[0], pmr[1]))))
+                             : m_max;
     lds_char_t* ob = smem + ((n + 1) & 1) * kQImg + 2 * (32 * w + r);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -412,7 +534,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       float lv = 0.f;
       __half mv = neg_inf_approx<__half>();
       if (l_tot > 0.f) {
-        mv = __float2half(m_max * kLn2);
+        mv = __float2half(m_fin * kLn2);
         // l relative to the STORED (rounded) m, so exp(s - m)/l is exact downstream
         lv = l_tot * __builtin_amdgcn_exp2f(m_run - __half2float(mv) * kLog2e);
       }
@@ -422,10 +544,10 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     }
   };
 
-  // Q chunks of the next item (one per phase, loaded at positions 2-5, stored two positions later)
-  u32x4 qst[2];
+  // the next item's Q chunk in flight (loaded at positions 2-5, stored one position later: one
+  // set of registers; the load has a whole position to land)
+  u32x4 qst;
   // the finished item's O / l / m leave from LDS at positions 2-3: lane constants
-  const int orow = tid >> 5, ocol = tid & 31;  // 16-B chunk (c = orow + 16j, queries 8*ocol..)
   const uint32_t osl = 2u * vd * nq;  // bytes per O slice
   const __amdgpu_buffer_rsrc_t ors = make_rsrc(static_cast<__half*>(a.O) + sl0 * (int64_t)vd * nq, osl * nsl);
   const __amdgpu_buffer_rsrc_t lrs = make_rsrc(static_cast<float*>(a.l) + sl0 * (int64_t)nq, 4u * nq * nsl);
@@ -480,18 +602,21 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // PV k-steps 2-3
     // staging: K(+3), V(+2) into the ring; loads of K(+5), V(+4) (this item's or the next's)
-    store(kOffK + ((c + 3) & 3) * kTile + kwo, kst[x]);
-    store(kOffV + ((c + 2) & 3) * kTile + vwo, vst[x]);
-    if constexpr (it >= 4 && it <= 7) {  // the next item's Q chunk j = it-4 over the finished item's O
-      uint32_t ql = ql_lane;
-      asm volatile("" : "+v"(ql));
-      store(((n + 1) & 1) * kQImg + ql + (it - 4) * 16 * kQRow, qst[x]);
+    if constexpr (!(F & kBANoStore)) {
+      store(kOffK + ((c + 3) & 3) * kTile + kwo, kst[x]);
+      store(kOffV + ((c + 2) & 3) * kTile + vwo, vst[x]);
     }
-    if constexpr (it == 2 || it == 3) {  // the finished item's O rows (at 2 also l / m); none before item 1
+    if constexpr (it >= 3 && it <= 6 && !(F & (kBANoItem | kBANoQ))) {
+      // the next item's Q chunk j = it-3 (channel rows 16j..16j+15) over the finished item's O,
+      // whose rows 16j.. both groups read out at MFMA(2 + j/2), an interval or more before
+      const int t = opaque_tid(), qc = t >> 5, qm2 = t & 31;
+      const uint32_t ql = qc * kQRow + ((qm2 * 16) ^ ((qc & 3) << 6));
+      store(((n + 1) & 1) * kQImg + ql + (it - 3) * 16 * kQRow, qst);
+    }
+    if constexpr ((it == 2 || it == 3) && !(F & (kBANoItem | kBANoOStore))) {  // the finished item's O rows (at 2 also l / m); none before item 1
       const bool on = prv_q0 < nq;
       const lds_char_t* ob = smem + ((n + 1) & 1) * kQImg;
-      int orw = orow, ocl = ocol, tt = tid;
-      asm volatile("" : "+v"(orw), "+v"(ocl), "+v"(tt));
+      const int tt = opaque_tid(), orw = tt >> 5, ocl = tt & 31;  // 16-B chunk (c = orw + 16j, queries 8*ocl..)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int cc = orw + 16 * (2 * (it & 1) + j);
@@ -508,11 +633,16 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         __builtin_amdgcn_raw_buffer_store_b128(v, mrs, moff, prv_sl * 2 * nq + 2 * min(prv_q0, nq), 0);
       }
     }
-    if constexpr (it >= 2 && it <= 5) qst[x] = qload(nxt, it - 2);
-    if constexpr (it + 5 < T) kst[x] = load(krs, koff, cur.sl * ksl, cur.kt0 + (it + 5) * kBN);
-    else kst[x] = load(krs, koff, nxt.sl * ksl, nxt.kt0 + (it + 5 - T) * kBN);
-    if constexpr (it + 4 < T) vst[x] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (it + 4) * kBN);
-    else vst[x] = load(vrs, voff, nxt.sl * vsl, nxt.kt0 + (it + 4 - T) * kBN);
+    if constexpr (it >= 2 && it <= 5 && !(F & (kBANoItem | kBANoQ))) qst = qload(nxt, it - 2);
+    if constexpr ((F & kBANoLoad) != 0) {  // timing ablation: every load re-reads tile 0 of slice 0
+      kst[x] = load(krs, koff, 0, 0);
+      vst[x] = load(vrs, voff, 0, 0);
+    } else {
+      if constexpr (it + 5 < T) kst[x] = load(krs, koff, cur.sl * ksl, cur.kt0 + (it + 5) * kBN);
+      else kst[x] = load(krs, koff, nxt.sl * ksl, nxt.kt0 + (it + 5 - T) * kBN);
+      if constexpr (it + 4 < T) vst[x] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (it + 4) * kBN);
+      else vst[x] = load(vrs, voff, nxt.sl * vsl, nxt.kt0 + (it + 4 - T) * kBN);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -523,16 +653,27 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's staging stores / reads landed
     if constexpr (it == 0) {
       if (n > 0) {
-        epilogue_lds();
+        if constexpr (!(F & (kBANoItem | kBANoEpi))) epilogue_lds();
         __builtin_amdgcn_sched_barrier(0);  // the epilogue's temporaries die before the softmax's
         m_max = kNegInf;
-        thr = -__FLT_MAX__;  // the item's first allowed key seeds m_run (scores are relative to it)
+        if constexpr (!PMAX) thr = kMaskFloor;  // the item's first allowed key seeds m_run (scores are relative to it)
         m_run = 0.f;         // (this item's first Sᵀ ran against -m = 0: see the end of VALU(T-1))
+        if constexpr (PMAX) {
+          pmr = half2v{(_Float16)0.f, (_Float16)0.f};
+          thr_h = (_Float16)-1.f;
+        }
         item_state(cur);
       }
     }
     const int cls = tcls(it);
-    if (cls != 0) {
+    if (cls != 0 && (F & kBANoSoftmax)) {  // timing ablation: P = S rounded, nothing else
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int z = 0; z < 4; ++z)
+          pw[y][z] = __builtin_bit_cast(uint32_t, half2v{(_Float16)st[y >> 1][8 * (y & 1) + 2 * z],
+                                                         (_Float16)st[y >> 1][8 * (y & 1) + 2 * z + 1]});
+    } else if (cls != 0) {
       softmax(it, cls, it == 0);
     } else {  // the next (unconditional) PV must add nothing
 #pragma unroll
@@ -646,17 +787,18 @@ bool fwd_f16_band_supported(const FwdArgs& a) {
   if ((nq + kBM - 1) / kBM > kMaxTab) return false;
   // one descriptor per tensor spans a workgroup's slices: below 2^31 bytes
   const int64_t nqb = (nq + kBM - 1) / kBM, n_items = a.b * nqb, n_wg = band_workgroups(n_items);
+  if (n_items >= (1ll << 31)) return false;  // the walk's item arithmetic is 32-bit
   const int xcds = device_xcds();
   const int64_t span =
       (band_interleaved(n_items, n_wg, xcds) ? (n_items + xcds - 1) / xcds : (n_items + n_wg - 1) / n_wg) / nqb + 2;
   return span * 2 * (int64_t)dm * (nq > nk ? nq : nk) < (1ll << 31);
 }
 
-template <int T, bool STAMP = false>
+template <int T, bool STAMP = false, int F = kBandDefault>
 hipError_t launch_band_t(const BandArgs& ba, hipStream_t s) {
-  hipError_t e = set_smem_once(reinterpret_cast<const void*>(fwd_f16_band_kernel<T, STAMP>), kSmem);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(fwd_f16_band_kernel<T, STAMP, F>), kSmem);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((fwd_f16_band_kernel<T, STAMP>), dim3((unsigned)ba.n_wg), dim3(kNW * 64), kSmem, s, ba);
+  hipLaunchKernelGGL((fwd_f16_band_kernel<T, STAMP, F>), dim3((unsigned)ba.n_wg), dim3(kNW * 64), kSmem, s, ba);
   return hipGetLastError();
 }
 
@@ -672,6 +814,20 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   const int dv = diag_variant("FA_FWD_VARIANT");
   if (dv == 2401 && ba.T == 12) return launch_band_t<12, true>(ba, s);
   if (dv == 2402) ba.inter = 0;  // round-2 order: contiguous runs of items
+  if (dv == 2403 && ba.T == 12) return launch_band_t<12, false, 0>(ba, s);  // round-2 softmax (exact max)
+  if (dv == 2404 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoMask>(ba, s);
+  if (dv == 2405 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoItem>(ba, s);
+  if (dv == 2406 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoSoftmax>(ba, s);
+  if (dv == 2408 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoLoad>(ba, s);
+  if (dv == 2409 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoStore>(ba, s);
+  if (dv == 2410 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoMask | kBANoItem | kBANoSoftmax | kBANoLoad | kBANoStore>(ba, s);
+  if (dv == 2411 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoEpi>(ba, s);
+  if (dv == 2412 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoOStore>(ba, s);
+  if (dv == 2413 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoQ>(ba, s);
+  if (dv == 2414 && ba.T == 12) return launch_band_t<12, false, kBANoEpi>(ba, s);
+  if (dv == 2415 && ba.T == 12) return launch_band_t<12, false, kBANoOStore>(ba, s);
+  if (dv == 2416 && ba.T == 12) return launch_band_t<12, false, kBANoQ>(ba, s);
+  if (dv == 2407 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoMask | kBANoItem | kBANoSoftmax>(ba, s);
 #endif
   switch (ba.T) {
     case 12: return launch_band_t<12>(ba, s);

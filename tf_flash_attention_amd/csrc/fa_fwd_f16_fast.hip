@@ -550,7 +550,7 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
     }
   }
   const bool tuned = v < 0;
-  if ((v == 2400 || v == 2401) && fwd_f16_band_supported(a)) return launch_fwd_f16_band(a, s);
+  if (v >= 2400 && v < 2500 && fwd_f16_band_supported(a)) return launch_fwd_f16_band(a, s);
 #else
   constexpr bool tuned = true;
 #endif
