@@ -5,7 +5,7 @@
 # Usage (GPU box): CONFIGS="c2 c3" bash tools/pmc_round.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-declare -A REGEX=([c2]=fwd_f16 [c3]="fwd_f16|bwd_dkdv|bwd_dq|bwd_prep" [c4]=fwd_f16 [c5]=fwd_f32_kernel)
+declare -A REGEX=([c2]=fwd_f16 [c3]="fwd_f16|bwd_dkdv|bwd_dq|bwd_prep" [c4]=fwd_f16 [c5]=fwd_f32_kernel [d32]=fwd_f16)
 G1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU"
 G2="SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT"
 G3="SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_WAVES"
