@@ -394,8 +394,7 @@ def test_config5_full2d_f32_sampled():
 #   with priority flips only, 2206 staging stores after the MFMAs, 2207 / 2208 fragment reads
 #   interleaved with the MFMAs (pairs / single MFMAs), 2213 the ping-pong default (2207 with the
 #   staging pinned too; forced here for causal / local, where the interleave is off), 2212
-#   ping-pong with LDS-DMA staging, 1814 the 8-wave forward that the ping-pong kernel replaced, and
-#   bwd 1281 the software-pipelined dK/dV pass (d = 128).
+#   ping-pong with LDS-DMA staging, 1814 the 8-wave forward that the ping-pong kernel replaced.
 @pytest.fixture
 def diag_lib(monkeypatch):
     """Routes the test through the diagnostic library (libfa_hip_diag.so), where the variant
@@ -440,22 +439,15 @@ def test_f16_forward_structures_d128(monkeypatch, diag_lib, variant, policy, seq
              bwd=False, seed=int(variant) + d + ws)
 
 
-# backward operand-read placement: 1200 = the d = 128 passes with reads beside their MFMAs (the
-# default before the run-ahead reads), 1410 = the dK/dV pass with P / dS formed by the consumer
-# waves, 1413 = its producer reading operands four k-steps ahead, 1500 / 1501 = the dQ pass's
-# staging (stores and loads / loads only) spread over its MFMA pairs, 1599 = the one-wave dQ pass, 1600 / 1601 / 1604 = the producer / consumer dQ pass, 1421 = both producer / consumer passes with the if-converted edge mask, 1430 = the dK/dV producer pre-reading the next tile
-# dQ pass, 1070 / 1071 = the d <= 64 passes with the if-converted edge mask / the dQ branch form, 1069 = the d <= 64 passes
-# with run-ahead reads
-@pytest.mark.parametrize("variant,d", [("1200", 128), ("1410", 128), ("1413", 128), ("1500", 128), ("1501", 128),
-                                       ("1599", 128), ("1600", 128), ("1601", 128), ("1604", 128), ("1421", 128), ("1430", 128), ("1069", 64), ("1069", 48), ("1070", 64), ("1071", 64)])
+# backward structures kept in the diagnostic library: 1599 = the one-wave dQ pass (the structure the
+# unaligned d > 64 shapes ship with) on aligned shapes, 1404 = the producer / consumer dK/dV pass's
+# stamp build (stamps go to the unused dQ workspace: gradients unchanged), 1068 / 1069 = the d <= 64
+# dQ pass with run-ahead operand reads, 1071 = its edge mask as a branch, 82 = the d <= 64 passes in
+# eight-wave blocks
+@pytest.mark.parametrize("variant,d", [("1599", 128), ("1404", 128), ("1068", 64), ("1069", 48), ("1071", 64),
+                                       ("82", 64)])
 @pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, True)])
 def test_f16_backward_read_placement(monkeypatch, diag_lib, variant, d, policy, ws, causal):
     monkeypatch.setenv("FA_BWD_VARIANT", variant)
     run_case(np.float16, policy, 1, "none_front", (2,), d, d, (328,), (264,), ws=ws, ls=0, causal=causal,
              seed=int(variant) + d)
-
-
-@pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, False)])
-def test_f16_backward_pipelined_dkdv(monkeypatch, diag_lib, policy, ws, causal):
-    monkeypatch.setenv("FA_BWD_VARIANT", "1281")
-    run_case(np.float16, policy, 1, "none_front", (2,), 128, 128, (328,), (264,), ws=ws, ls=0, causal=causal, seed=7)

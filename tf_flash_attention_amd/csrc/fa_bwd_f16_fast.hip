@@ -95,19 +95,13 @@ struct DkdvSmem {
 };
 
 // ---------------------------------------------------------------------------
-// dK / dV: key-outer.
-// PIPE (one wave per SIMD, registers to spare): software-pipelined over query tiles with a
-// 3-slot ring — the S / dP MFMAs of tile it+1 are issued beside the softmax of tile it, then
-// the dV / dK MFMAs of tile it; the LDS latency of one tile's operand reads and the VALU
-// work hide under the other tile's MFMAs (a single wave per SIMD has nothing else to hide
-// them behind).  One workgroup = NW waves x 32 keys of one (batch, head) slice.
-// ablation bits (timing diagnostics, outputs WRONG; FA_BWD_VARIANT=1300+bits, d = 128):
-// 1 no exp2, 2 no tile stores, 4 no tile loads, 8 no Q/dO transposed reads, 16 no G-image reads, 32 no barrier
-template <int D, int NW, int WPE, int POL, bool ALN, bool PIPE = false, int ABL = 0>
+// dK / dV: key-outer.  One workgroup = NW waves x 32 keys of one (batch, head) slice (the d <= 64
+// pass, two waves per SIMD; d = 128 runs the producer / consumer pass below).
+template <int D, int NW, int WPE, int POL, bool ALN>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
-  using S = DkdvSmem<D, NW, PIPE ? 3 : 2>;
+  using S = DkdvSmem<D, NW>;
   constexpr int kThr = NW * 64;
   constexpr int kBK = S::kBK;
   constexpr int kQChunks = D * 4;                     // 16-B chunks of one [D][32] tile
@@ -276,49 +270,16 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       }
     }
   };
-  // ABL bit 64 (not an ablation): the operand reads of sdp / dvdk run two k-steps ahead of their
-  // MFMAs (one wave per SIMD: nothing else hides an LDS round trip between a read and its MFMA)
-  constexpr bool PRE = (ABL & 64) != 0;
-  constexpr int kAh = (ABL & 128) ? 3 : 2;  // run-ahead distance (MFMA pairs)
   // S = Qᵀ·K', dP = dOᵀ·V: A operands (row q, k = channel) by transposed reads
-  auto sdp_pre = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) __attribute__((always_inline)) {
-    constexpr int kS = D / 16;
-    half8 qa8[kAh + 1], oa8[kAh + 1];
-    auto rd = [&](int s) __attribute__((always_inline)) {
+  auto sdp = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) {
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      half8 qa8, oa8;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const uint32_t off = q16_off(16 * s + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
         const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
-        if (e == 0) { qa8[s % (kAh + 1)].lo = x; oa8[s % (kAh + 1)].lo = y; } else { qa8[s % (kAh + 1)].hi = x; oa8[s % (kAh + 1)].hi = y; }
-      }
-    };
-#pragma unroll
-    for (int s = 0; s < kAh; ++s) rd(s);
-#pragma unroll
-    for (int s = 0; s < kS; ++s) {
-      if (s + kAh < kS) rd(s + kAh);
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8[s % (kAh + 1)], kb[s], sacc, 0, 0, 0);
-      pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8[s % (kAh + 1)], vb[s], pacc, 0, 0, 0);
-    }
-  };
-  auto sdp = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) {
-    if constexpr (PRE) {
-      sdp_pre(base, sacc, pacc);
-      return;
-    }
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      half8 qa8, oa8;
-      if (ABL & 8) {
-        qa8 = kb[(s + 1) % (D / 16)];
-        oa8 = vb[(s + 1) % (D / 16)];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const uint32_t off = q16_off(16 * s + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
-          const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
-          if (e == 0) { qa8.lo = x; oa8.lo = y; } else { qa8.hi = x; oa8.hi = y; }
-        }
+        if (e == 0) { qa8.lo = x; oa8.lo = y; } else { qa8.hi = x; oa8.hi = y; }
       }
       sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8, kb[s], sacc, 0, 0, 0);
       pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8, vb[s], pacc, 0, 0, 0);
@@ -329,7 +290,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float pv = (ABL & 1) ? sacc[i] : __builtin_amdgcn_exp2f(sacc[i]);
+      float pv = __builtin_amdgcn_exp2f(sacc[i]);
       if (POL == 1 && masked) {
         const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
         pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
@@ -342,9 +303,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       sf[i >> 3][i & 7] = (_Float16)(pv * pacc[i]);
     }
   };
-  // the edge-tile mask as a real branch (see the producer / consumer pass; ABL & 512: the if-converted form)
+  // the edge-tile mask as a real branch (see the producer / consumer pass)
   auto softmax = [&](const floatx16& sacc, const floatx16& pacc, int qa, int cls, half8 (&pf)[2], half8 (&sf)[2]) {
-    if constexpr ((ABL & 512) != 0 || POL == 0) {
+    if constexpr (POL == 0) {
       softmax_m(sacc, pacc, qa, cls == 1, pf, sf);
     } else if (cls == 1) {
       asm volatile("; edge tile" ::: );
@@ -356,114 +317,48 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   };
   // dV += dO·P, dK += Q·dS: A = X[row 32u + r][queries 16s + 8h + 0..7] (b128 reads of the Q16 images)
   auto dvdk = [&](const lds_char_t* base, const half8 (&pf)[2], const half8 (&sf)[2]) {
-    if constexpr (PRE) {
-      constexpr int kU = D / 32, kN = 2 * kU;  // (s, u) pairs, n = s * kU + u
-      half8 oa[kAh + 1], qa[kAh + 1];
-      auto rd = [&](int n) __attribute__((always_inline)) {
-        const int s_ = n / kU, u = n % kU;
-        oa[n % (kAh + 1)] = read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s_ + h));
-        qa[n % (kAh + 1)] = read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s_ + h));
-      };
-#pragma unroll
-      for (int n = 0; n < kAh; ++n) rd(n);
-#pragma unroll
-      for (int n = 0; n < kN; ++n) {
-        if (n + kAh < kN) rd(n + kAh);
-        const int s_ = n / kU, u = n % kU;
-        dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa[n % (kAh + 1)], pf[s_], dv[u], 0, 0, 0);
-        dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[n % (kAh + 1)], sf[s_], dk[u], 0, 0, 0);
-      }
-      return;
-    }
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int u = 0; u < D / 32; ++u) {
-        const half8 oa = (ABL & 16) ? vb[2 * s + u] : read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s + h));
-        const half8 qa = (ABL & 16) ? kb[2 * s + u] : read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s + h));
+        const half8 oa = read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s + h));
+        const half8 qa = read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s + h));
         dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa, pf[s], dv[u], 0, 0, 0);
         dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa, sf[s], dk[u], 0, 0, 0);
       }
   };
 
-  if constexpr (!PIPE) {
-    load_tile(qt0, 0);  // unconditional, as in the dQ pass
-    store_tile(0, 0);
-    load_tile(qt0 + 32, 1);
-    load_tile(qt0 + 64, 0);
+  load_tile(qt0, 0);  // unconditional, as in the dQ pass
+  store_tile(0, 0);
+  load_tile(qt0 + 32, 1);
+  load_tile(qt0 + 64, 0);
 
-    // iteration it: tile it in slot it&1 (complete after the barrier); tile it+1 -> slot (it+1)&1
-    // (read in iteration it-1, finished before this barrier) from staging set (it+1)&1, which then
-    // takes tile it+3.  Loads and stores are unconditional (past the end they move zeros into
-    // a slot nobody reads), so hipcc's vmcnt waits stay exact: a store waits only for the load
-    // issued two steps earlier.
-    auto step = [&](auto P_, int it) {
-      constexpr int p = decltype(P_)::value;
-      if (!(ABL & 32)) __syncthreads();
-      const int qa = qt0 + 32 * it;
-      if (!(ABL & 2)) store_tile(p ^ 1, p ^ 1);
-      if (!(ABL & 4)) load_tile(qa + 96, p ^ 1);
-      const int cls = it < ntiles ? tcls(qa) : 0;  // (the loop's last pair may end on a phantom step)
-      if (cls == 0) return;
-      const lds_char_t* base = smem + p * S::kSlot;
-      floatx16 sacc, pacc;
-      init_acc(base, sacc, pacc);
-      sdp(base, sacc, pacc);
-      half8 pf[2], sf[2];
-      softmax(sacc, pacc, qa, cls, pf, sf);
-      dvdk(base, pf, sf);
-    };
-    // whole pairs of steps: a conditional second step (it loads) made hipcc's vmcnt waits before the
-    // staging stores drain every load in flight, the one issued a step earlier included
-    for (int it = 0; it < ntiles; it += 2) {
-      step(IC<0>{}, it);
-      step(IC<1>{}, it + 1);
-    }
-  } else {
-    // tile j lives in slot j % 3; step it: barrier (tile it+1 complete), tile it+2 -> slot
-    // (it+2)%3 (tile it-1's, finished in step it-1), tile it+3 -> registers; S/dP(it+1) beside
-    // the softmax of tile it; dV/dK(it)
-    if (ntiles > 0) { load_tile(qt0, 0); store_tile(0, 0); }
-    if (ntiles > 1) { load_tile(qt0 + 32, 0); store_tile(1, 0); }
-    if (ntiles > 2) load_tile(qt0 + 64, 0);
+  // iteration it: tile it in slot it&1 (complete after the barrier); tile it+1 -> slot (it+1)&1
+  // (read in iteration it-1, finished before this barrier) from staging set (it+1)&1, which then
+  // takes tile it+3.  Loads and stores are unconditional (past the end they move zeros into
+  // a slot nobody reads), so hipcc's vmcnt waits stay exact: a store waits only for the load
+  // issued two steps earlier.
+  auto step = [&](auto P_, int it) {
+    constexpr int p = decltype(P_)::value;
     __syncthreads();
-    floatx16 sa, pa, sb, pb;  // S / dP accumulators of two consecutive tiles
-    if (ntiles > 0 && tcls(qt0) != 0) {
-      init_acc(smem, sa, pa);
-      sdp(smem, sa, pa);
-    }
-    auto step = [&](auto C_, auto Q_, int it, floatx16& scur, floatx16& pcur, floatx16& snxt, floatx16& pnxt) {
-      constexpr int c = decltype(C_)::value;  // it mod 3
-      __syncthreads();
-      const int qa = qt0 + 32 * it;
-      if (it + 2 < ntiles) store_tile((c + 2) % 3, 0);
-      if (it + 3 < ntiles) load_tile(qa + 96, 0);
-      const int cls = tcls(qa);
-      const int cls1 = (it + 1 < ntiles) ? tcls(qa + 32) : 0;
-      const lds_char_t* base = smem + c * S::kSlot;
-      const lds_char_t* base1 = smem + ((c + 1) % 3) * S::kSlot;
-      half8 pf[2], sf[2];
-      if (cls1 != 0 && cls != 0) {  // one basic block: tile it+1's MFMAs beside tile it's softmax
-        init_acc(base1, snxt, pnxt);
-        sdp(base1, snxt, pnxt);
-        softmax(scur, pcur, qa, cls, pf, sf);
-      } else {
-        if (cls1 != 0) {
-          init_acc(base1, snxt, pnxt);
-          sdp(base1, snxt, pnxt);
-        }
-        if (cls != 0) softmax(scur, pcur, qa, cls, pf, sf);
-      }
-      if (cls != 0) dvdk(base, pf, sf);
-    };
-    for (int it = 0; it < ntiles; it += 6) {
-      step(IC<0>{}, IC<0>{}, it, sa, pa, sb, pb);
-      if (it + 1 < ntiles) step(IC<1>{}, IC<1>{}, it + 1, sb, pb, sa, pa);
-      if (it + 2 < ntiles) step(IC<2>{}, IC<0>{}, it + 2, sa, pa, sb, pb);
-      if (it + 3 < ntiles) step(IC<0>{}, IC<1>{}, it + 3, sb, pb, sa, pa);
-      if (it + 4 < ntiles) step(IC<1>{}, IC<0>{}, it + 4, sa, pa, sb, pb);
-      if (it + 5 < ntiles) step(IC<2>{}, IC<1>{}, it + 5, sb, pb, sa, pa);
-    }
+    const int qa = qt0 + 32 * it;
+    store_tile(p ^ 1, p ^ 1);
+    load_tile(qa + 96, p ^ 1);
+    const int cls = it < ntiles ? tcls(qa) : 0;  // (the loop's last pair may end on a phantom step)
+    if (cls == 0) return;
+    const lds_char_t* base = smem + p * S::kSlot;
+    floatx16 sacc, pacc;
+    init_acc(base, sacc, pacc);
+    sdp(base, sacc, pacc);
+    half8 pf[2], sf[2];
+    softmax(sacc, pacc, qa, cls, pf, sf);
+    dvdk(base, pf, sf);
+  };
+  // whole pairs of steps: a conditional second step (it loads) made hipcc's vmcnt waits before the
+  // staging stores drain every load in flight, the one issued a step earlier included
+  for (int it = 0; it < ntiles; it += 2) {
+    step(IC<0>{}, it);
+    step(IC<1>{}, it + 1);
   }
 
   // ---- dK = scale·Σ dS·Q, dV: rows c = 32u + (i&3) + 8(i>>2) + 4h, column = this lane's key
@@ -505,7 +400,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 // producer, the dK / dV accumulators in the consumer, each role inside its own loop so neither
 // carries the other's registers (under 256 each at D = 128).  Every step: one barrier, the
 // staging of tile i+1 into the ring, the load of tile i+3.
-template <int D, bool SMX = false>
+template <int D>
 struct PcSmem {
   static constexpr int kBK = 128;            // keys per workgroup: four producer waves x 32
   static constexpr int kRow = D * kBK * 2;   // K (or V) row image (prologue only)
@@ -514,7 +409,7 @@ struct PcSmem {
   static constexpr int kSlot = offLse + 2 * 32 * 4;  // + -lse2[32], -D[32]
   static constexpr int kNS = 4;              // query-tile ring
   static constexpr int offX = kNS * kSlot;   // P / dS hand-over: 2 slots x 4 waves x 4 KB
-  static constexpr int kXWave = SMX ? 8192 : 4096;  // (SMX: raw fp32 S and dP, 8 KB a wave)
+  static constexpr int kXWave = 4096;
   static constexpr int kXSlot = 4 * kXWave;
   static constexpr int kUsed = offX + 2 * kXSlot;
   static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;  // the K/V images alias the ring
@@ -524,18 +419,12 @@ template <int D, int POL, bool ALN, int PF = 0>
 __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
-  // PF & 64 (SMX): the producer hands over its raw fp32 S and dP; the consumer, which otherwise
-  // waits at the barrier for about half of each step, forms P = exp2(S) and dS = P∘dP itself
-  constexpr bool SMX = (PF & 64) != 0;
-  using S = PcSmem<D, SMX>;
+  using S = PcSmem<D>;
   constexpr int kThr = 512;
   constexpr int kBK = S::kBK;
   constexpr int kQChunks = D * 4;                 // 16-B chunks of one [D][32] tile
   static_assert((2 * kQChunks) % kThr == 0, "tile chunks must divide over the workgroup");
   constexpr int kCPT = 2 * kQChunks / kThr;       // Q and dO chunks per thread
-  // PF & 2: two barriers per step — phase A: the producer's S / dP MFMAs (the consumer stages and
-  // reads its operands), phase B: the producer's softmax beside the consumer's dV / dK MFMAs
-  constexpr bool TWO = (PF & 2) != 0;
   // PF & 4 (diagnostic build): per-wave s_memtime sums of each step's parts (stage + barrier, MFMA
   // part, softmax / hand-over part) written to the unused dQ workspace
   constexpr bool STAMP = (PF & 4) != 0;
@@ -683,35 +572,19 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   // compile-time); loads and stores are unconditional (phantom tiles move zeros), so hipcc's vmcnt
   // waits stay exact.
   const int nsteps = ntiles + 1;
-  // PF & 512 (AHD): tiles stored two steps ahead (tile it+2 in step it, loads four ahead), so the
-  // producer reads the next tile's row constants and first operands before the step's barrier
-  constexpr bool AHD = (PF & 512) != 0;
   auto stage = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;
     __syncthreads();
-    if constexpr (AHD) {
-      store_tile((c + 2) % 4, c % 2);               // tile it+2 (loaded in step it-2)
-      load_tile(qt0 + 32 * (it + 4), c % 2);        // tile it+4 into the set just stored
-    } else {
-      store_tile((c + 1) % 4, (c + 1) % 2);         // tile it+1 (loaded in step it-2)
-      load_tile(qt0 + 32 * (it + 3), (c + 1) % 2);  // tile it+3 into the set just stored
-    }
+    store_tile((c + 1) % 4, (c + 1) % 2);         // tile it+1 (loaded in step it-2)
+    load_tile(qt0 + 32 * (it + 3), (c + 1) % 2);  // tile it+3 into the set just stored
   };
   // first tiles: tile 0's loads issued now, its store after the barrier that retires the K/V images
   load_tile(qt0, 0);
-  if constexpr (AHD) load_tile(qt0 + 32, 1);
   auto stage0 = [&]() __attribute__((always_inline)) {
     __syncthreads();
     store_tile(0, 0);
-    if constexpr (AHD) {
-      store_tile(1, 1);
-      load_tile(qt0 + 64, 0);
-      load_tile(qt0 + 96, 1);
-      __syncthreads();  // tiles 0 and 1 published: the producer pre-reads tile 0
-    } else {
-      load_tile(qt0 + 32, 1);
-      load_tile(qt0 + 64, 0);
-    }
+    load_tile(qt0 + 32, 1);
+    load_tile(qt0 + 64, 0);
   };
 
   if (grp == 0) {
@@ -755,19 +628,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
         if (e == 0) { q8.lo = x; o8.lo = y; } else { q8.hi = x; o8.hi = y; }
       }
     };
-    floatx16 nsacc, npacc;  // AHD: the next tile's row constants and first two k-steps' operands
-    half8 nq8[2], no8[2];
-    auto preread = [&](int slot, int itn) __attribute__((always_inline)) {
-      if constexpr (AHD) {
-        const int cl = itn < ntiles ? tcls(qt0 + 32 * itn) : 0;
-        if (cl == 0) return;
-        const lds_char_t* base = smem + slot * S::kSlot;
-        read_rowc(base, nsacc, npacc);
-#pragma unroll
-        for (int s_ = 0; s_ < 2; ++s_) read_ops(base, s_, nq8[s_], no8[s_]);
-      }
-    };
-    preread(0, 0);
     auto pstep = [&](auto C_, int it) __attribute__((always_inline)) {
       constexpr int c = decltype(C_)::value;
       stamp(-1);
@@ -779,43 +639,23 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       floatx16 sacc, pacc;
       if (cls != 0) {
         // S = Qᵀ·K', dP = dOᵀ·V: A operands by transposed reads, two k-steps ahead of their MFMAs
-        // (PF & 128: four ahead)
-        constexpr int kS = D / 16, kAh = (PF & 128) ? 4 : 2;
+        constexpr int kS = D / 16, kAh = 2;
         half8 qa8[kAh + 1], oa8[kAh + 1];
         auto rd = [&](int s_) __attribute__((always_inline)) {
           read_ops(base, s_, qa8[s_ % (kAh + 1)], oa8[s_ % (kAh + 1)]);
         };
-        if constexpr (AHD) {  // read before the barrier (end of the previous step)
-          sacc = nsacc;
-          pacc = npacc;
+        read_rowc(base, sacc, pacc);
 #pragma unroll
-          for (int s_ = 0; s_ < 2; ++s_) { qa8[s_] = nq8[s_]; oa8[s_] = no8[s_]; }
-        } else {
-          read_rowc(base, sacc, pacc);
-#pragma unroll
-          for (int s_ = 0; s_ < kAh; ++s_) rd(s_);
-        }
-        if constexpr ((PF & 1) != 0) __builtin_amdgcn_s_setprio(1);  // the S / dP MFMAs first; the consumer's fill in
+        for (int s_ = 0; s_ < kAh; ++s_) rd(s_);
 #pragma unroll
         for (int s_ = 0; s_ < kS; ++s_) {
           if (s_ + kAh < kS) rd(s_ + kAh);
           sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8[s_ % (kAh + 1)], kb[s_], sacc, 0, 0, 0);
           pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8[s_ % (kAh + 1)], vb[s_], pacc, 0, 0, 0);
         }
-        if constexpr ((PF & 1) != 0) __builtin_amdgcn_s_setprio(0);
       }
       stamp(1);
-      if constexpr (TWO) __builtin_amdgcn_s_barrier();  // phase B: this softmax beside the consumer's MFMAs
       if (cls == 0) return;
-      if constexpr (SMX) {  // raw S (chunks 0-3) and dP (4-7), four registers a chunk, lane-linear
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          *reinterpret_cast<lds_f4_t*>(smem + xoff(c % 2, j)) = floatx4{sacc[4 * j], sacc[4 * j + 1], sacc[4 * j + 2], sacc[4 * j + 3]};
-          *reinterpret_cast<lds_f4_t*>(smem + xoff(c % 2, 4 + j)) = floatx4{pacc[4 * j], pacc[4 * j + 1], pacc[4 * j + 2], pacc[4 * j + 3]};
-        }
-        stamp(2);
-        return;
-      }
       // P = exp2(S), dS = P∘dP; register i = query 16(i>>3) + 8h + (i&7) = k-step i>>3 of the consumer
       half8 pf[2], sf[2];
       auto softmax = [&](bool masked) __attribute__((always_inline)) {
@@ -835,10 +675,8 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
         }
       };
       // the edge-tile mask as a real branch: in one basic block hipcc if-converts it into an index add,
-      // a compare and two selects per score on every tile (PF & 256: that form, for A/B)
-      if constexpr ((PF & 256) != 0) {
-        softmax(cls == 1);
-      } else if (POL != 0 && cls == 1) {
+      // a compare and two selects per score on every tile (c3 backward 8.35 -> 7.72 ms)
+      if (POL != 0 && cls == 1) {
         asm volatile("; edge tile" ::: );
         softmax(true);
       } else {
@@ -852,23 +690,17 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       }
       stamp(2);
     };
-    auto pstep2 = [&](auto C_, int it) __attribute__((always_inline)) {
-      constexpr int c = decltype(C_)::value;
-      pstep(C_, it);
-      preread((c + 1) % 4, it + 1);  // (AHD: tile it+1 was stored in step it-1, published by this step's barrier)
-    };
     for (int it = 0; it < nsteps; it += 4) {
-      pstep2(IC<0>{}, it);
-      pstep2(IC<1>{}, it + 1);
-      pstep2(IC<2>{}, it + 2);
-      pstep2(IC<3>{}, it + 3);
+      pstep(IC<0>{}, it);
+      pstep(IC<1>{}, it + 1);
+      pstep(IC<2>{}, it + 2);
+      pstep(IC<3>{}, it + 3);
     }
     stamp_out();
     return;
   }
 
   // ================= consumer
-  const int kord = (POL == 2 && SMX) ? seq_order(a.rule.k, a.rule, min(key, nk - 1)) : 0;
   stage0();
   floatx16 dk[D / 32], dv[D / 32];
 #pragma unroll
@@ -891,49 +723,19 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       oa[n % (kAh + 1)] = read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s_ + h));
       qa_[n % (kAh + 1)] = read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s_ + h));
     };
-    // SMX: P and dS of k-step s_ (registers i = 8 s_ + jj of the producer's S / dP) formed here
-    auto smx = [&](int s_) __attribute__((always_inline)) {
-      const int xs = (c + 1) % 2;
-      const floatx4 s0 = *reinterpret_cast<const lds_f4_t*>(smem + xoff(xs, 2 * s_));
-      const floatx4 s1 = *reinterpret_cast<const lds_f4_t*>(smem + xoff(xs, 2 * s_ + 1));
-      const floatx4 d0 = *reinterpret_cast<const lds_f4_t*>(smem + xoff(xs, 4 + 2 * s_));
-      const floatx4 d1 = *reinterpret_cast<const lds_f4_t*>(smem + xoff(xs, 5 + 2 * s_));
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const float sv = jj < 4 ? s0[jj] : s1[jj - 4], dpv = jj < 4 ? d0[jj] : d1[jj - 4];
-        float pv = __builtin_amdgcn_exp2f(sv);
-        if (POL == 1 && cls == 1) {
-          const int q = qa + 16 * s_ + 8 * h + jj;
-          pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
-        }
-        if (POL == 2 && cls == 1) {
-          const int q = qa + 16 * s_ + 8 * h + jj;
-          pv = (q < nq && check_orders_bf(a.rule, seq_order(a.rule.q, a.rule, min(q, nq - 1)), kord)) ? pv : 0.f;
-        }
-        pf[s_][jj] = (_Float16)pv;
-        sf[s_][jj] = (_Float16)(pv * dpv);
-      }
-    };
     if (cls != 0) {
-      if constexpr (!SMX) {
 #pragma unroll
-        for (int s_ = 0; s_ < 2; ++s_) {
-          pf[s_] = read_b128(smem + xoff((c + 1) % 2, s_));
-          sf[s_] = read_b128(smem + xoff((c + 1) % 2, 2 + s_));
-        }
+      for (int s_ = 0; s_ < 2; ++s_) {
+        pf[s_] = read_b128(smem + xoff((c + 1) % 2, s_));
+        sf[s_] = read_b128(smem + xoff((c + 1) % 2, 2 + s_));
       }
 #pragma unroll
       for (int n = 0; n < kAh; ++n) rd(n);
     }
     stamp(1);
-    if constexpr (TWO) __builtin_amdgcn_s_barrier();  // phase B: these MFMAs beside the producer's softmax
     if (cls == 0) return;
-    if constexpr (SMX) smx(0);
 #pragma unroll
     for (int n = 0; n < kN; ++n) {
-      if constexpr (SMX) {
-        if (n == 1) smx(1);  // k-step 1's P / dS beside k-step 0's MFMAs
-      }
       if (n + kAh < kN) rd(n + kAh);
       const int s_ = n / kU, u = n % kU;
       dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa[n % (kAh + 1)], pf[s_], dv[u], 0, 0, 0);
@@ -990,7 +792,7 @@ struct DqSmem {
 };
 
 // dQ: query-outer.  One workgroup = NW waves x 32 queries of one (batch, head) slice.
-template <int D, int NW, int WPE, int POL, bool ALN, bool PRE = false, int SPR = 0, bool MSPEC = false>
+template <int D, int NW, int WPE, int POL, bool ALN, bool PRE = false, bool MSPEC = false>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -1139,20 +941,6 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
       *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[set][j];
     }
   };
-  // SPR: one chunk's store and re-load at a time, between the Sᵀ / dPᵀ MFMA pairs (one wave per SIMD:
-  // a 1 KB load or a 16-B-per-lane store issued at the step head holds the wave for tens of cycles
-  // each while the matrix pipe idles)
-  auto stage_chunk = [&](int slot, int set, int j, int ka) __attribute__((always_inline)) {
-    const bool isV = is_v(j);
-    if constexpr (SPR == 1)
-      *reinterpret_cast<lds_u32x4_t*>(smem + slot * S::kSlot + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[set][j];
-    const bool out = ka + 8 * cm >= nk;
-    if constexpr (ALN)
-      kr[set][j] = buf_load16(isV ? vrs : krs, voff[j], 2 * min(ka, nk), out || crow_[j] >= (isV ? vd : d));
-    else
-      kr[set][j] = buf_load8h(isV ? vrs : krs, voff[j], ka + 8 * cm, nk, crow_[j] < (isV ? vd : d));
-  };
-
   floatx16 dq[D / 32];
 #pragma unroll
   for (int u = 0; u < D / 32; ++u)
@@ -1185,11 +973,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     const int ka = kt0 + it * kBN;
     const int cls = it < ntiles ? tcls(ka) : 0;  // (the loop's last pair may end on a phantom step)
     // unconditional (past the end they move zeros into a slot nobody reads): exact vmcnt waits
-    if (SPR == 2 || (SPR != 0 && cls == 0)) store_tile(p ^ 1, p ^ 1);  // (SPR 2: the loads alone spread)
-    if (SPR == 0 || cls == 0) {
-      if (SPR == 0) store_tile(p ^ 1, p ^ 1);
-      load_tile(ka + 3 * kBN, p ^ 1);
-    }
+    store_tile(p ^ 1, p ^ 1);
+    load_tile(ka + 3 * kBN, p ^ 1);
     if (cls == 0) return;
     const lds_char_t* base = smem + p * S::kSlot;
     floatx16 st[2], dp[2];
@@ -1212,12 +997,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
       };
       rd(0);
       rd(1);
-      static_assert(!SPR || kN % kCPT == 0, "staging chunks spread over the MFMA pairs");
 #pragma unroll
       for (int n = 0; n < kN; ++n) {
-        if constexpr (SPR) {
-          if (n % (kN / kCPT) == 0) stage_chunk(p ^ 1, p ^ 1, n / (kN / kCPT), ka + 3 * kBN);
-        }
         if (n + 2 < kN) rd(n + 2);
         if (n == kN - 2) rka(0);
         if (n == kN - 1) rka(1);
@@ -1333,14 +1114,11 @@ struct DqPcSmem {
   static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;  // the Q/dO images alias the ring
 };
 
-// PF & 4 (CDP): the consumer forms dPᵀ and dSᵀ, the producer only Sᵀ and Pᵀ (hands over fp16 Pᵀ) and
-// stages the key tiles: 16 + 32 MFMAs instead of 32 + 16.  PF & 1: the producer's MFMAs at priority 1.
-template <int D, int POL, bool ALN, int PF = 0>
+template <int D, int POL, bool ALN>
 __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
   using S = DqPcSmem<D>;
-  constexpr bool CDP = (PF & 4) != 0;
   constexpr int kThr = 512, kHalfThr = 256;  // one half of the workgroup stages
   constexpr int kBM = S::kBM, kBN = 64;
   constexpr int kKChunks = D * 8;  // 16-B chunks of one [D][64] tile
@@ -1423,15 +1201,13 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
     if (wlo_min > kz || whi_max < ka) return 0;
     return (wlo_max <= ka && whi_min >= kz && kz < nk) ? 2 : 1;
   };
-  // hand-over slot of this wave pair: k-steps 0..3 of dSᵀ (or of Pᵀ under CDP), one b128 each, lane-linear
+  // hand-over slot of this wave pair: k-steps 0..3 of dSᵀ, one b128 each, lane-linear
   auto xoff = [&](int xs, int j) -> uint32_t { return S::offX + xs * S::kXSlot + wl * S::kXWave + j * 1024 + lane * 16; };
   // Steps it = 0 .. ntiles: the producer handles tile it (it < ntiles), the consumer tile it-1 (it >= 1),
   // in whole groups of four (ring slot it % 4, staging set (it+1) % 2, hand-over slot it % 2 compile-time)
   const int nsteps = ntiles + 1;
 
-  // ---- key-tile staging (K, V chunks: 8 keys of one channel row) by one half of the workgroup:
-  // the consumers (default) or, under CDP, the producers
-  const bool stager = (grp == 1) != CDP;
+  // ---- key-tile staging (K, V chunks: 8 keys of one channel row) by the consumer half of the workgroup
   const int ct = tid & (kHalfThr - 1);
   const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + bi * (int64_t)d * nk, 2u * d * nk);
   const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk, 2u * vd * nk);
@@ -1481,10 +1257,8 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
     load_tile(kt0 + kBN, 1);
     load_tile(kt0 + 2 * kBN, 0);
   };
-  (void)stager;
-
-  // resident B operands, lane (r,h) holds X[c = 16s + 8h + j][q = wq0 + r]: Q' in the producer,
-  // dO in the producer (default) or the consumer (CDP); the row constants likewise
+  // resident B operands of the producer, lane (r,h) holds X[c = 16s + 8h + j][q = wq0 + r]: Q' and dO;
+  // the row constants likewise
   auto resident = [&](int img, half8* x) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < D / 16; ++s)
@@ -1552,37 +1326,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) qf[s] = scale8(qf[s], c2);
     const floatx16 negl = rowconst(a.ws_lse, kNegInf);
-    if constexpr (CDP) {
-      load_tile(kt0, 0);                   // (tile 0's loads before the barrier that retires the images)
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every image read done before the ring reuses it
-      stage0();
-      auto pstep = [&](auto C_, int it) __attribute__((always_inline)) {
-        constexpr int c = decltype(C_)::value;
-        stage(C_, it);
-        const int ka = kt0 + it * kBN;
-        const int cls = it < ntiles ? tcls(ka) : 0;
-        if (cls == 0) return;
-        const lds_char_t* base = smem + c * S::kSlot;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const floatx16 st = half_chain(base + S::offKT, qf, negl, t);
-#pragma unroll
-          for (int sh = 0; sh < 2; ++sh) {
-            half8 pf;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) pf[j] = (_Float16)pval(st[8 * sh + j], cls, ka, t, 8 * sh + j);
-            *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, 2 * t + sh)) = pf;
-          }
-        }
-      };
-      for (int it = 0; it < nsteps; it += 4) {
-        pstep(IC<0>{}, it);
-        pstep(IC<1>{}, it + 1);
-        pstep(IC<2>{}, it + 2);
-        pstep(IC<3>{}, it + 3);
-      }
-      return;
-    } else {
+    {
       half8 of[D / 16];
       resident(1, of);
       const floatx16 negd = rowconst(a.ws_D, 0.f);
@@ -1597,10 +1341,8 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
         const lds_char_t* base = smem + c * S::kSlot;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {  // one 32-key half at a time: 16 MFMAs, then its two dSᵀ k-steps
-          if constexpr ((PF & 1) != 0) __builtin_amdgcn_s_setprio(1);
           const floatx16 st = half_chain(base + S::offKT, qf, negl, t);
           const floatx16 dp = half_chain(base + S::offVT, of, negd, t);
-          if constexpr ((PF & 1) != 0) __builtin_amdgcn_s_setprio(0);
           auto softmax = [&](int cl) __attribute__((always_inline)) {
 #pragma unroll
             for (int sh = 0; sh < 2; ++sh) {
@@ -1610,10 +1352,8 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
               *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, 2 * t + sh)) = dsf;
             }
           };
-          // the edge-tile mask as a real branch (see the dK/dV pass; PF & 8: the if-converted form)
-          if constexpr ((PF & 8) != 0) {
-            softmax(cls);
-          } else if (cls == 1) {
+          // the edge-tile mask as a real branch (see the dK/dV pass)
+          if (cls == 1) {
             asm volatile("; edge tile" ::: );
             softmax(1);
           } else {
@@ -1632,18 +1372,9 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
     }
   }
 
-  // ================= consumer: dQ += K·dSᵀ for tile it-1 (CDP: dPᵀ and dSᵀ = Pᵀ∘dPᵀ formed here)
-  half8 of[CDP ? D / 16 : 1];
-  floatx16 negd;
-  if constexpr (CDP) {
-    resident(1, of);
-    negd = rowconst(a.ws_D, 0.f);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __syncthreads();  // (stage0 of the producers)
-  } else {
-    load_tile(kt0, 0);
-    stage0();
-  }
+  // ================= consumer: dQ += K·dSᵀ for tile it-1; it stages the key tiles
+  load_tile(kt0, 0);
+  stage0();
   floatx16 dq[D / 32];
 #pragma unroll
   for (int u = 0; u < D / 32; ++u)
@@ -1662,16 +1393,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
     half8 dsf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) dsf[s] = read_b128(smem + xoff((c + 1) % 2, s));
-    if constexpr (CDP) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const floatx16 dp = half_chain(base + S::offVT, of, negd, t);
-#pragma unroll
-        for (int sh = 0; sh < 2; ++sh)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) dsf[2 * t + sh][j] = (_Float16)((float)dsf[2 * t + sh][j] * dp[8 * sh + j]);
-      }
-    }
     constexpr int kN = 4 * (D / 32);
     half8 ka8p[3];
     auto rka = [&](int n) __attribute__((always_inline)) {  // operand n = (D/32)·s + u, two ahead
@@ -1686,15 +1407,9 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
       dq[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka8p[n % 3], dsf[s], dq[u], 0, 0, 0);
     }
   };
-  // PF & 16 (SLATE): the consumer's dQ MFMAs right after the barrier, its staging after them
   auto cstep = [&](auto C_, int it) __attribute__((always_inline)) {
-    constexpr int c = decltype(C_)::value;
-    if constexpr (CDP || (PF & 16) != 0) __syncthreads(); else stage(C_, it);
+    stage(C_, it);
     cwork(C_, it);
-    if constexpr (!CDP && (PF & 16) != 0) {
-      store_tile((c + 1) % 4, (c + 1) % 2);
-      load_tile(kt0 + kBN * (it + 3), (c + 1) % 2);
-    }
   };
   for (int it = 0; it < nsteps; it += 4) {
     cstep(IC<0>{}, it);
@@ -1737,18 +1452,18 @@ inline bool bwd_aligned(const BwdArgs& a) {
 }
 using BwdKernel = void (*)(BwdArgs);
 
-template <int D, int NW, int WPE, bool PIPE = false, int ABL = 0>
+template <int D, int NW, int WPE>
 hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
-  using S = DkdvSmem<D, NW, PIPE ? 3 : 2>;
+  using S = DkdvSmem<D, NW>;
   const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
   const int pol = bwd_pol(a.rule);
   const BwdKernel kern =
-      bwd_aligned(a) ? (pol == 0   ? bwd_dkdv_kernel<D, NW, WPE, 0, true, PIPE, ABL>
-                        : pol == 1 ? bwd_dkdv_kernel<D, NW, WPE, 1, true, PIPE, ABL>
-                                   : bwd_dkdv_kernel<D, NW, WPE, 2, true, PIPE, ABL>)
-                     : (pol == 0   ? bwd_dkdv_kernel<D, NW, WPE, 0, false, PIPE, ABL>
-                        : pol == 1 ? bwd_dkdv_kernel<D, NW, WPE, 1, false, PIPE, ABL>
-                                   : bwd_dkdv_kernel<D, NW, WPE, 2, false, PIPE, ABL>);
+      bwd_aligned(a) ? (pol == 0   ? bwd_dkdv_kernel<D, NW, WPE, 0, true>
+                        : pol == 1 ? bwd_dkdv_kernel<D, NW, WPE, 1, true>
+                                   : bwd_dkdv_kernel<D, NW, WPE, 2, true>)
+                     : (pol == 0   ? bwd_dkdv_kernel<D, NW, WPE, 0, false>
+                        : pol == 1 ? bwd_dkdv_kernel<D, NW, WPE, 1, false>
+                                   : bwd_dkdv_kernel<D, NW, WPE, 2, false>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(NW * 64), S::kTotal, s, a);
@@ -1757,7 +1472,7 @@ hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
 
 template <int D, int PF = 0>
 hipError_t launch_dkdv_pc(const BwdArgs& a, hipStream_t s) {
-  using S = PcSmem<D, (PF & 64) != 0>;
+  using S = PcSmem<D>;
   const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
   const int pol = bwd_pol(a.rule);
   const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dkdv_pc_kernel<D, 0, true, PF>
@@ -1772,34 +1487,34 @@ hipError_t launch_dkdv_pc(const BwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int D, int NW, int WPE, bool PRE = false, int SPR = 0, bool MSPEC = false>
+template <int D, int NW, int WPE, bool PRE = false, bool MSPEC = false>
 hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
   using S = DqSmem<D, NW>;
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
   const int pol = bwd_pol(a.rule);
-  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, true, PRE, SPR, MSPEC>
-                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, true, PRE, SPR, MSPEC>
-                                                      : bwd_dq_kernel<D, NW, WPE, 2, true, PRE, SPR, MSPEC>)
-                                        : (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, false, PRE, SPR, MSPEC>
-                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, false, PRE, SPR, MSPEC>
-                                                      : bwd_dq_kernel<D, NW, WPE, 2, false, PRE, SPR, MSPEC>);
+  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, true, PRE, MSPEC>
+                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, true, PRE, MSPEC>
+                                                      : bwd_dq_kernel<D, NW, WPE, 2, true, PRE, MSPEC>)
+                                        : (pol == 0   ? bwd_dq_kernel<D, NW, WPE, 0, false, PRE, MSPEC>
+                                           : pol == 1 ? bwd_dq_kernel<D, NW, WPE, 1, false, PRE, MSPEC>
+                                                      : bwd_dq_kernel<D, NW, WPE, 2, false, PRE, MSPEC>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(NW * 64), S::kTotal, s, a);
   return hipGetLastError();
 }
 
-template <int D, int PF = 0>
+template <int D>
 hipError_t launch_dq_pc(const BwdArgs& a, hipStream_t s) {
   using S = DqPcSmem<D>;
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
   const int pol = bwd_pol(a.rule);
-  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_pc_kernel<D, 0, true, PF>
-                                           : pol == 1 ? bwd_dq_pc_kernel<D, 1, true, PF>
-                                                      : bwd_dq_pc_kernel<D, 2, true, PF>)
-                                        : (pol == 0   ? bwd_dq_pc_kernel<D, 0, false, PF>
-                                           : pol == 1 ? bwd_dq_pc_kernel<D, 1, false, PF>
-                                                      : bwd_dq_pc_kernel<D, 2, false, PF>);
+  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_pc_kernel<D, 0, true>
+                                           : pol == 1 ? bwd_dq_pc_kernel<D, 1, true>
+                                                      : bwd_dq_pc_kernel<D, 2, true>)
+                                        : (pol == 0   ? bwd_dq_pc_kernel<D, 0, false>
+                                           : pol == 1 ? bwd_dq_pc_kernel<D, 1, false>
+                                                      : bwd_dq_pc_kernel<D, 2, false>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(512), S::kTotal, s, a);
@@ -1824,75 +1539,33 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
 #ifdef FA_DIAG
-  // FA_BWD_VARIANT selects A/B structures (82, 1067-1069, 1200, 1264, 1265, 1267, 1281, 1400-1403) and the
-  // d = 128 dK/dV ablations 1301-1363 (outputs WRONG)
+  // FA_BWD_VARIANT (diagnostic library): d <= 64 — 82 eight-wave blocks, 1068 / 1069 the dQ pass's
+  // operand reads run ahead, 1071 its edge mask as a branch; d = 128 — 1404 the dK/dV pass's stamp
+  // build (tools/pc_stamps.py), 1599 the one-wave dQ pass (the unaligned shapes' structure) on
+  // aligned shapes.  The rest of round 2's A/B variants were measured and removed.
   const int v = diag_variant("FA_BWD_VARIANT");
   if (max(a.d, a.v_d) <= 64 && v >= 0) {
-    switch (v) {
-      case 82: e = launch_dkdv<64, 8, 2>(a, s); break;
-      case 1070: e = launch_dkdv<64, 4, 2, false, 512>(a, s); break;  // the edge mask if-converted (before)
-      case 1067: case 1069: e = launch_dkdv<64, 4, 2, false, 64>(a, s); break;
-      default: e = launch_dkdv<64, 4, 2>(a, s); break;
-    }
+    e = v == 82 ? launch_dkdv<64, 8, 2>(a, s) : launch_dkdv<64, 4, 2>(a, s);
     if (e != hipSuccess) return e;
     switch (v) {
-      case 82: return launch_dq<64, 8, 2, false, 0, true>(a, s);
+      case 82: return launch_dq<64, 8, 2, false, true>(a, s);
       case 1068: case 1069: return launch_dq<64, 4, 2, true>(a, s);
-      case 1071: return launch_dq<64, 4, 2>(a, s);  // the dQ pass with the edge-mask branch (spills)
-      default: return launch_dq<64, 4, 2, false, 0, true>(a, s);
+      case 1071: return launch_dq<64, 4, 2>(a, s);
+      default: return launch_dq<64, 4, 2, false, true>(a, s);
     }
   }
   if (max(a.d, a.v_d) > 64 && v >= 0) {
-    switch (v) {
-      case 1400: e = launch_dkdv_pc<128>(a, s); break;
-      case 1265: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;  // round-2 default (one wave per SIMD)
-      case 1401: e = launch_dkdv_pc<128, 1>(a, s); break;
-      case 1402: e = launch_dkdv_pc<128, 2>(a, s); break;
-      case 1403: e = launch_dkdv_pc<128, 3>(a, s); break;
-      case 1404: e = launch_dkdv_pc<128, 4>(a, s); break;  // stamps into the dQ workspace (tools/pc_stamps.py)
-      case 1406: e = launch_dkdv_pc<128, 6>(a, s); break;
-      case 1410: e = launch_dkdv_pc<128, 64>(a, s); break;  // the softmax on the consumer side
-      case 1411: e = launch_dkdv_pc<128, 64 | 4>(a, s); break;
-      case 1412: e = launch_dkdv_pc<128, 64 | 1>(a, s); break;
-      case 1413: e = launch_dkdv_pc<128, 128>(a, s); break;  // producer operand reads four k-steps ahead
-      case 1420: e = launch_dkdv_pc<128, 256>(a, s); break;  // the edge mask if-converted (before)
-      case 1430: e = launch_dkdv_pc<128, 512>(a, s); break;  // tiles stored two ahead, producer pre-reads
-      case 1421: e = launch_dkdv_pc<128, 256>(a, s); break;  // (with 1608's dQ pass)
-      case 1414: e = launch_dkdv_pc<128, 128 | 4>(a, s); break;
-      case 1281: e = launch_dkdv<128, 4, 1, true>(a, s); break;
-      case 1200: e = launch_dkdv<128, 4, 1>(a, s); break;  // operand reads not run ahead (before the default)
-      case 1264: e = launch_dkdv<128, 4, 1, false, 64>(a, s); break;
-      case 1267: e = launch_dkdv<128, 4, 1, false, 64 | 128>(a, s); break;
-      case 1301: e = launch_dkdv<128, 4, 1, false, 1>(a, s); break;
-      case 1302: e = launch_dkdv<128, 4, 1, false, 2>(a, s); break;
-      case 1304: e = launch_dkdv<128, 4, 1, false, 4>(a, s); break;
-      case 1308: e = launch_dkdv<128, 4, 1, false, 8>(a, s); break;
-      case 1316: e = launch_dkdv<128, 4, 1, false, 16>(a, s); break;
-      case 1324: e = launch_dkdv<128, 4, 1, false, 24>(a, s); break;
-      case 1338: e = launch_dkdv<128, 4, 1, false, 38>(a, s); break;
-      case 1363: e = launch_dkdv<128, 4, 1, false, 63>(a, s); break;
-      default: e = launch_dkdv_pc<128>(a, s); break;
-    }
+    e = v == 1404 ? launch_dkdv_pc<128, 4>(a, s) : launch_dkdv_pc<128>(a, s);
     if (e != hipSuccess) return e;
-    if (v == 1200 || v == 1264) return launch_dq<128, 4, 1>(a, s);
-    if (v == 1599) return launch_dq<128, 4, 1, true>(a, s);  // the one-wave dQ pass (default before 1600)
-    if (v == 1500) return launch_dq<128, 4, 1, true, 1>(a, s);  // staging spread over the MFMA pairs
-    if (v == 1501) return launch_dq<128, 4, 1, true, 2>(a, s);  // ... the loads only
-    if (v == 1600) return launch_dq_pc<128>(a, s);  // producer / consumer dQ pass
-    if (v == 1601) return launch_dq_pc<128, 1>(a, s);  // ... the producer's MFMAs at priority 1
-    if (v == 1604) return launch_dq_pc<128, 4>(a, s);  // ... dPᵀ / dSᵀ formed by the consumer
-    if (v == 1608) return launch_dq_pc<128, 8>(a, s);  // ... the edge mask if-converted (before)
-    if (v == 1616) return launch_dq_pc<128, 16>(a, s);  // ... the consumer's staging after its MFMAs
-    if (v == 1421) return launch_dq_pc<128, 8>(a, s);
-    if (bwd_aligned(a)) return launch_dq_pc<128>(a, s);
-    return launch_dq<128, 4, 1, true>(a, s);
+    if (v == 1599 || !bwd_aligned(a)) return launch_dq<128, 4, 1, true>(a, s);
+    return launch_dq_pc<128>(a, s);
   }
 #endif
   if (max(a.d, a.v_d) <= 64) {
     e = launch_dkdv<64, 4, 2>(a, s);
     if (e != hipSuccess) return e;
     // (the d <= 64 dQ pass keeps the if-converted edge mask: the branch form spills 8-42 VGPRs there)
-    return launch_dq<64, 4, 2, false, 0, true>(a, s);
+    return launch_dq<64, 4, 2, false, true>(a, s);
   }
   // tuned (c3): the producer / consumer dK/dV pass (one-process A/B: 9.20 -> 8.59 ms backward; two
   // barriers per step, 1402, and a prioritised producer, 1401, measured 8.70 / 8.77) and, for 16-B
