@@ -67,12 +67,58 @@ constexpr int kMinT = 12;
 // structure flags: the rebase check and m on the packed P (fa_fwd_f16_pingpong.hip's kFPMax; the
 // default since round 3; 0 = round 2's exact fp32 row max on every tile)
 constexpr int kBFPMax = 1;
-constexpr int kBandDefault = kBFPMax;
 // timing ablations (diagnostic library only; outputs WRONG): no edge masks, no softmax (P = S
 // rounded), every staging load re-reading one hot tile (L2-resident), no staging LDS stores.  (An
 // ablation that drops the output — the O epilogue — lets hipcc delete the PV work with it, so the
 // item-boundary traffic has none.)
 constexpr int kBANoMask = 2, kBANoSoftmax = 8, kBANoLoad = 16, kBANoStore = 32;
+// one staging register set: the K / V loads run one position ahead of their store instead of two
+constexpr int kBLead1 = 64;
+// staggered groups: group 1 (queries 128-255 of the item) works on tile p + 2 where group 0 works on
+// tile p, so an item is T' positions for T' + 2 tiles instead of T positions for T tiles (a 256-query
+// item of a ws = 256 band: 10 positions instead of 12; each group's four waves span 10 tiles).  The
+// stream stages 1.2 tiles a position (two at the item boundary, see stag_k / stag_v), loads one
+// position ahead of their store.
+constexpr int kBStag = 128;
+constexpr int kMinTStag = 10;
+constexpr int kMaxTStag = 22;
+constexpr int kBandDefault = kBFPMax | kBStag;  // round 3: staggered groups
+constexpr int kBandR3 = kBFPMax;                // round 3 before the stagger: T positions for T tiles
+
+// staggered staging schedule (T positions, NT = T + 2 tiles an item, rings of four slots: tile j in
+// slot j & 3).  Tile j of an item is read by group 0 as K at position j (j < T) and as V at j + 1, by
+// group 1 as K at j - 2 and as V at j - 1 (j >= 2).  A group's chunk of a tile is stored in its MFMA
+// phase of position p (interval 2p + g), visible two intervals later, and only after every read of
+// the slot's previous tile (j - 4).  Entry i (0, 1) of the tiles group g stores at position p;
+// indices >= NT are the next item's tile index - NT; -1 none.  A group with one tile where the
+// other has two repeats it (the same chunk to the same place: the pair runs branch-free).
+__host__ __device__ constexpr int stag_k1(int T, int p, int g, int i) {
+  const int NT = T + 2;
+  if (g == 0) {
+    if (p == 0) return i == 0 ? 1 : 3;
+    if (p <= T - 2) return p + 3;
+    return i == 0 ? NT : NT + 2;
+  }
+  if (p == 0) return 3;
+  if (p <= T - 3) return p + 3;
+  if (p == T - 2) return i == 0 ? T + 1 : NT;
+  return i == 0 ? NT + 1 : NT + 2;
+}
+__host__ __device__ constexpr int stag_v1(int T, int p, int g, int i) {
+  const int NT = T + 2;
+  if (g == 0) {
+    if (p == 0) return i == 0 ? 0 : 2;
+    if (p == 1) return i == 0 ? 1 : 3;
+    return p + 2;
+  }
+  if (p == 0) return i == 0 ? 1 : 2;
+  if (p == 1) return 3;
+  if (p <= T - 2) return p + 2;
+  return i == 0 ? T + 1 : NT;
+}
+// tiles (per group) stored at position p: two at the item boundary, one elsewhere
+__host__ __device__ constexpr int stag_nk(int T, int p) { return (p == 0 || p >= T - 2) ? 2 : 1; }
+__host__ __device__ constexpr int stag_nv(int T, int p) { return (p <= 1 || p == T - 1) ? 2 : 1; }
 constexpr float kRescaleThr = 8.f;
 // masked scores sit at or below -2^19 (the arithmetic edge mask); a row maximum at or below this
 // floor means "nothing allowed yet" (never a reference), and is the unset state of thr
@@ -109,13 +155,16 @@ struct Item {
 template <int T, bool STAMP = false, int F = kBandDefault>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) {
   constexpr bool PMAX = (F & kBFPMax) != 0;
+  constexpr bool STG = (F & kBStag) != 0;
+  constexpr int NT = STG ? T + 2 : T;  // tiles an item streams
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
   const FwdArgs& a = ba.a;
   constexpr float kNegInf = -__builtin_huge_valf();
 
   const int nq = a.rule.q.n, nk = a.rule.k.n;
-  static_assert(T % 4 == 0 && T >= kMinT, "T: a multiple of 4, at least kMinT");
+  static_assert(STG ? ((T + 2) % 4 == 0 && T >= kMinTStag) : (T % 4 == 0 && T >= kMinT),
+                "T: a multiple of 4 (staggered: T + 2), at least kMinT (kMinTStag)");
   const int nqb = (nq + kBM - 1) / kBM;
   // this workgroup's items: first + stride * local, inside [it_begin, it_end).
   //   contiguous: a run of consecutive items per workgroup (stride 1);
@@ -142,6 +191,8 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = w >> 2;  // waves w and w+4 share a SIMD
+  const int toff = STG ? 2 * grp : 0;  // staggered: this group's tile at position p is p + toff
   const int h = lane >> 5, r = lane & 31;
   const int gq = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const int d = a.d, vd = a.v_d;
@@ -160,9 +211,19 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   // into LDS, so the stream's item switch is a table read, not two binary searches
   const lds_char_t* tab = smem + kOffTab;
   for (int qb = threadIdx.x; qb < nqb; qb += kNW * 64) {
-    int kb, ke;
-    k_range_for_q_block(a.rule, qb * kBM, min(qb * kBM + kBM, nq) - 1, &kb, &ke);
-    *reinterpret_cast<__attribute__((address_space(3))) int*>(smem + kOffTab + 4 * qb) = (kb / kBN) * kBN;
+    int kb, ke, kt;
+    if constexpr (STG) {  // the first tile group 0 needs, and two before group 1's first (may be < 0)
+      k_range_for_q_block(a.rule, qb * kBM, min(qb * kBM + kBM / 2, nq) - 1, &kb, &ke);
+      kt = ke > kb ? (kb / kBN) * kBN : nk;
+      if (qb * kBM + kBM / 2 < nq) {
+        k_range_for_q_block(a.rule, qb * kBM + kBM / 2, min(qb * kBM + kBM, nq) - 1, &kb, &ke);
+        if (ke > kb) kt = min(kt, (kb / kBN) * kBN - 2 * kBN);
+      }
+    } else {
+      k_range_for_q_block(a.rule, qb * kBM, min(qb * kBM + kBM, nq) - 1, &kb, &ke);
+      kt = (kb / kBN) * kBN;
+    }
+    *reinterpret_cast<__attribute__((address_space(3))) int*>(smem + kOffTab + 4 * qb) = kt;
   }
   __syncthreads();
   // the walk's item index n = first + local * stride as (slice, query block), advanced by
@@ -204,6 +265,10 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   const uint32_t kwo = crow * 128 + ((cm * 16) ^ ((crow & 2) << 5));
   const uint32_t vwo = crow * 128 + 16 * (cm ^ ((crow >> 1) & 7));
   auto load = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t slb, int k0) -> u32x4 __attribute__((always_inline)) {
+    if constexpr (STG) {  // (staggered items may start before key 0: those tiles read zeros)
+      const bool in = k0 >= 0 && k0 + 8 * cm < nk;
+      return __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off : 0x80000000u, slb + 2 * min(max(k0, 0), nk), 0);
+    }
     const bool in = k0 + 8 * cm < nk;
     return __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off : 0x80000000u, slb + 2 * min(k0, nk), 0);
   };
@@ -240,8 +305,13 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     for (int j = 0; j < 2; ++j) vp[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + j * kBN);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (3 + j) * kBN);
-      vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (2 + j) * kBN);
+      if constexpr (STG) {  // the chunks this thread's group stores at position 0
+        kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 0, 1, j) : stag_k1(T, 0, 0, j)) * kBN);
+        vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 0, 1, j) : stag_v1(T, 0, 0, j)) * kBN);
+      } else {
+        kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (3 + j) * kBN);
+        vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (2 + j) * kBN);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) qv[j] = qload(cur, j);
@@ -249,8 +319,15 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     for (int j = 0; j < 4; ++j) store(ql_lane + j * 16 * kQRow, qv[j]);
 #pragma unroll
     for (int j = 0; j < 3; ++j) store(kOffK + j * kTile + kwo, kp[j]);
+    if constexpr (STG) {
+      // staggered: K(0..2) and V(0) are the tiles the schedule stores before position 0; V slots 1 and
+      // 3 feed the first PV of each group (P = 0) and are zeroed
+      store(kOffV + vwo, vp[0]);
+      store(kOffV + kTile + 16 * tid, u32x4{0, 0, 0, 0});
+    } else {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) store(kOffV + j * kTile + vwo, vp[j]);
+      for (int j = 0; j < 2; ++j) store(kOffV + j * kTile + vwo, vp[j]);
+    }
     store(kOffV + 3 * kTile + 16 * tid, u32x4{0, 0, 0, 0});
   }
   __syncthreads();
@@ -558,11 +635,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   // at 2-3 and into LDS at 4-5)
   auto mfma_phase = [&](auto IT_) __attribute__((always_inline)) {
     constexpr int it = decltype(IT_)::value;
-    constexpr int c = it & 3, x = it & 1;
+    constexpr bool L1 = (F & kBLead1) != 0;
+    constexpr int c = it & 3, x = L1 ? 0 : it & 1, kA = L1 ? 4 : 5;  // kA: the K tile loaded, positions ahead
     __builtin_amdgcn_s_setprio(1);
-    const lds_char_t* pk = smem + kOffK + c * kTile;
-    const lds_char_t* pkn = smem + kOffK + ((c + 1) & 3) * kTile;
-    const lds_char_t* pv = smem + kOffV + ((c + 3) & 3) * kTile;
+    // (staggered: this group's tiles are p + toff, toff in {0, 2}, tile j in slot j & 3, and
+    // (j + toff) & 3 = (j & 3) ^ toff; the PV at position 0 is of the previous item's tile T-1+toff)
+    constexpr int cv = (STG && it == 0) ? ((T - 1) & 3) : ((c + 3) & 3);
+    const lds_char_t* pk = smem + kOffK + (STG ? (c ^ toff) : c) * kTile;
+    const lds_char_t* pv = smem + kOffV + (STG ? (cv ^ toff) : cv) * kTile;
     // every fragment is read in the phase that uses it, two k-steps ahead (nothing lives across
     // the VALU phase: the register budget holds the stream's staging); the first two K k-steps
     // are read at the phase start, their latency the only one exposed
@@ -600,7 +680,20 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // PV k-steps 2-3
     // staging: K(+3), V(+2) into the ring; loads of K(+5), V(+4) (this item's or the next's)
-    if constexpr (!(F & kBANoStore)) {
+    if constexpr (STG) {  // the group's tiles of this position (stag_k1 / stag_v1), tile j in slot j & 3
+      if constexpr (!(F & kBANoStore)) {
+        static_for<0, stag_nk(T, it)>([&](auto I_) __attribute__((always_inline)) {
+          constexpr int i = decltype(I_)::value, j0 = stag_k1(T, it, 0, i), j1 = stag_k1(T, it, 1, i);
+          const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
+          store(kOffK + (j & 3) * kTile + kwo, kst[i]);
+        });
+        static_for<0, stag_nv(T, it)>([&](auto I_) __attribute__((always_inline)) {
+          constexpr int i = decltype(I_)::value, j0 = stag_v1(T, it, 0, i), j1 = stag_v1(T, it, 1, i);
+          const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
+          store(kOffV + (j & 3) * kTile + vwo, vst[i]);
+        });
+      }
+    } else if constexpr (!(F & kBANoStore)) {
       store(kOffK + ((c + 3) & 3) * kTile + kwo, kst[x]);
       store(kOffV + ((c + 2) & 3) * kTile + vwo, vst[x]);
     }
@@ -632,14 +725,36 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       }
     }
     if constexpr (it >= 2 && it <= 5) qst = qload(nxt, it - 2);
-    if constexpr ((F & kBANoLoad) != 0) {  // timing ablation: every load re-reads tile 0 of slice 0
+    if constexpr (STG) {
+      // the chunks the group stores at the next position (the next item's position 0 at T-1), one
+      // position ahead; tile j of the current item, or j - NT of the next
+      constexpr int pn = it + 1 < T ? it + 1 : 0, add = it + 1 < T ? 0 : NT;
+      auto src = [&](int j0, int j1, uint32_t slsz, int& slb, int& k0) __attribute__((always_inline)) {
+        const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
+        const bool nx = j >= NT;
+        slb = (nx ? nxt.sl : cur.sl) * (int)slsz;
+        k0 = (nx ? nxt.kt0 : cur.kt0) + (nx ? j - NT : j) * kBN;
+      };
+      static_for<0, stag_nk(T, pn)>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = decltype(I_)::value;
+        int slb, k0;
+        src(stag_k1(T, pn, 0, i) + add, stag_k1(T, pn, 1, i) + add, ksl, slb, k0);
+        kst[i] = load(krs, koff, (uint32_t)slb, k0);
+      });
+      static_for<0, stag_nv(T, pn)>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = decltype(I_)::value;
+        int slb, k0;
+        src(stag_v1(T, pn, 0, i) + add, stag_v1(T, pn, 1, i) + add, vsl, slb, k0);
+        vst[i] = load(vrs, voff, (uint32_t)slb, k0);
+      });
+    } else if constexpr ((F & kBANoLoad) != 0) {  // timing ablation: every load re-reads tile 0 of slice 0
       kst[x] = load(krs, koff, 0, 0);
       vst[x] = load(vrs, voff, 0, 0);
     } else {
-      if constexpr (it + 5 < T) kst[x] = load(krs, koff, cur.sl * ksl, cur.kt0 + (it + 5) * kBN);
-      else kst[x] = load(krs, koff, nxt.sl * ksl, nxt.kt0 + (it + 5 - T) * kBN);
-      if constexpr (it + 4 < T) vst[x] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (it + 4) * kBN);
-      else vst[x] = load(vrs, voff, nxt.sl * vsl, nxt.kt0 + (it + 4 - T) * kBN);
+      if constexpr (it + kA < T) kst[x] = load(krs, koff, cur.sl * ksl, cur.kt0 + (it + kA) * kBN);
+      else kst[x] = load(krs, koff, nxt.sl * ksl, nxt.kt0 + (it + kA - T) * kBN);
+      if constexpr (it + kA - 1 < T) vst[x] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (it + kA - 1) * kBN);
+      else vst[x] = load(vrs, voff, nxt.sl * vsl, nxt.kt0 + (it + kA - 1 - T) * kBN);
     }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -663,7 +778,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         item_state(cur);
       }
     }
-    const int cls = tcls(it);
+    const int cls = tcls(it + toff);
     if (cls != 0 && (F & kBANoSoftmax)) {  // timing ablation: P = S rounded, nothing else
 #pragma unroll
       for (int y = 0; y < 4; ++y)
@@ -672,7 +787,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
           pw[y][z] = __builtin_bit_cast(uint32_t, half2v{(_Float16)st[y >> 1][8 * (y & 1) + 2 * z],
                                                          (_Float16)st[y >> 1][8 * (y & 1) + 2 * z + 1]});
     } else if (cls != 0) {
-      softmax(it, cls, it == 0);
+      softmax(it + toff, cls, it == 0);
     } else {  // the next (unconditional) PV must add nothing
 #pragma unroll
       for (int y = 0; y < 4; ++y)
@@ -693,7 +808,6 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     }
   };
 
-  const int grp = w >> 2;  // waves w and w+4 share a SIMD
   if (grp == 1) __builtin_amdgcn_s_barrier();
   // diagnostic build only (STAMP): s_memtime of waves 0 and 4 of workgroup 0 at the four phase
   // edges of every position of its first four items, written over the last slice's Q (WRONG)
@@ -745,7 +859,7 @@ struct TCache {
   int T;
   bool valid;
 };
-thread_local TCache g_tcache = {{}, 0, false};
+thread_local TCache g_tcache = {{}, 0, false}, g_scache = {{}, 0, false};
 
 }  // namespace
 
@@ -767,6 +881,32 @@ int band_tiles_per_item(const FwdArgs& a) {
   return T;
 }
 
+// staggered items (kBStag): positions T' an item takes when group 1 runs two tiles ahead of group 0
+// (the first tile two before group 1's first allowed key or at group 0's, whichever is lower); T' + 2
+// a multiple of 4, at least kMinTStag
+int band_positions_stag(const FwdArgs& a) {
+  if (g_scache.valid && !memcmp(&g_scache.r, &a.rule, sizeof(Rule))) return g_scache.T;
+  const int nq = a.rule.q.n, nk = a.rule.k.n;
+  const int nqb = (nq + kBM - 1) / kBM;
+  int T = 0;
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int q0 = qb * kBM;
+    int kb0, ke0, kb1 = 0, ke1 = 0;
+    k_range_for_q_block(a.rule, q0, min(q0 + kBM / 2, nq) - 1, &kb0, &ke0);
+    const bool g1 = q0 + kBM / 2 < nq;
+    if (g1) k_range_for_q_block(a.rule, q0 + kBM / 2, min(q0 + kBM, nq) - 1, &kb1, &ke1);
+    int kt = ke0 > kb0 ? (kb0 / kBN) * kBN : nk;
+    if (g1 && ke1 > kb1) kt = min(kt, (kb1 / kBN) * kBN - 2 * kBN);
+    if (ke0 > kb0) T = max(T, (ke0 - kt + kBN - 1) / kBN);
+    if (g1 && ke1 > kb1) T = max(T, (ke1 - kt + kBN - 1) / kBN - 2);
+  }
+  T = (max(T, kMinTStag) + 2 + 3) / 4 * 4 - 2;
+  g_scache.r = a.rule;
+  g_scache.T = T;
+  g_scache.valid = true;
+  return T;
+}
+
 bool fwd_f16_band_supported(const FwdArgs& a) {
   const Rule& r = a.rule;
   const int nq = r.q.n, nk = r.k.n;
@@ -780,7 +920,7 @@ bool fwd_f16_band_supported(const FwdArgs& a) {
       (reinterpret_cast<uintptr_t>(a.Q) % 16) || nq % 8)
     return false;
   // a band: every block spans few tiles (else the per-launch kernels cover it at no loss)
-  if (band_tiles_per_item(a) > 24) return false;
+  if (band_positions_stag(a) > kMaxTStag) return false;
   // the per-slice table of first key tiles lives in LDS: kMaxTab query blocks (nq <= 1M)
   if ((nq + kBM - 1) / kBM > kMaxTab) return false;
   // one descriptor per tensor spans a workgroup's slices: below 2^31 bytes
@@ -803,26 +943,45 @@ hipError_t launch_band_t(const BandArgs& ba, hipStream_t s) {
 hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   BandArgs ba;
   ba.a = a;
-  ba.T = band_tiles_per_item(a);
+  ba.T = band_positions_stag(a);
   ba.n_items = a.b * (int64_t)((a.rule.q.n + kBM - 1) / kBM);
   ba.n_wg = (int)band_workgroups(ba.n_items);
   ba.n_xcd = device_xcds();
   ba.inter = band_interleaved(ba.n_items, ba.n_wg, ba.n_xcd) ? 1 : 0;
 #ifdef FA_DIAG
+  // FA_FWD_VARIANT: 2400 the unstaggered structure (T positions for T tiles), 2401 its stamp build,
+  // 2402 either with the contiguous item order, 2403-2410 its ablations / A-B (T = 12 only), 2421
+  // the staggered stamp build (T' = 10)
   const int dv = diag_variant("FA_FWD_VARIANT");
-  if (dv == 2401 && ba.T == 12) return launch_band_t<12, true>(ba, s);
   if (dv == 2402) ba.inter = 0;  // round-2 order: contiguous runs of items
-  if (dv == 2403 && ba.T == 12) return launch_band_t<12, false, 0>(ba, s);  // round-2 softmax (exact max)
-  if (dv == 2404 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoMask>(ba, s);
-  if (dv == 2406 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoSoftmax>(ba, s);
-  if (dv == 2408 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoLoad>(ba, s);
-  if (dv == 2409 && ba.T == 12) return launch_band_t<12, false, kBandDefault | kBANoStore>(ba, s);
+  if (dv >= 2400 && dv < 2420 && dv != 2402) {
+    ba.T = band_tiles_per_item(a);
+    if (ba.T == 12) {
+      switch (dv) {
+        case 2401: return launch_band_t<12, true, kBandR3>(ba, s);
+        case 2403: return launch_band_t<12, false, 0>(ba, s);  // round-2 softmax (exact max)
+        case 2404: return launch_band_t<12, false, kBandR3 | kBANoMask>(ba, s);
+        case 2406: return launch_band_t<12, false, kBandR3 | kBANoSoftmax>(ba, s);
+        case 2408: return launch_band_t<12, false, kBandR3 | kBANoLoad>(ba, s);
+        case 2409: return launch_band_t<12, false, kBandR3 | kBANoStore>(ba, s);
+        case 2410: return launch_band_t<12, false, kBandR3 | kBLead1>(ba, s);
+        default: break;
+      }
+    }
+    switch (ba.T) {
+      case 12: return launch_band_t<12, false, kBandR3>(ba, s);
+      case 16: return launch_band_t<16, false, kBandR3>(ba, s);
+      case 20: return launch_band_t<20, false, kBandR3>(ba, s);
+      default: return launch_band_t<24, false, kBandR3>(ba, s);
+    }
+  }
+  if (dv == 2421 && ba.T == 10) return launch_band_t<10, true>(ba, s);
 #endif
   switch (ba.T) {
-    case 12: return launch_band_t<12>(ba, s);
-    case 16: return launch_band_t<16>(ba, s);
-    case 20: return launch_band_t<20>(ba, s);
-    default: return launch_band_t<24>(ba, s);
+    case 10: return launch_band_t<10>(ba, s);
+    case 14: return launch_band_t<14>(ba, s);
+    case 18: return launch_band_t<18>(ba, s);
+    default: return launch_band_t<22>(ba, s);
   }
 }
 

@@ -1,6 +1,8 @@
-"""Phase timeline of the persistent band forward (diagnostic library, FA_FWD_VARIANT=2401):
-s_memtime of waves 0 (group 0) and 4 (group 1) of workgroup 0 at the four phase edges of every
-position of its first four items (written over the last slice's Q; outputs WRONG).  Usage: python tools/band_stamps.py"""
+"""Phase timeline of the persistent band forward (diagnostic library; FA_FWD_VARIANT=2421 the
+staggered default, T = 10 positions an item; 2401 the unstaggered structure, T = 12): s_memtime of
+waves 0 (group 0) and 4 (group 1) of workgroup 0 at the four phase edges of every position of its
+first four items (written over the last slice's Q; outputs WRONG).
+Usage: python tools/band_stamps.py [variant [T]]"""
 import os
 import sys
 
@@ -24,10 +26,10 @@ def main():
     v = (torch.rand((b, d) + ks, device=dev) * 4 - 2).to(dt)
     for _ in range(200):  # clock ramp
         fa.attention_forward(policy, seq_dims, q, k, v, sync, ws, ls, causal)
-    os.environ["FA_FWD_VARIANT"] = "2401"
+    os.environ["FA_FWD_VARIANT"] = sys.argv[1] if len(sys.argv) > 1 else "2421"
     fa.attention_forward(policy, seq_dims, q, k, v, sync, ws, ls, causal)
     torch.cuda.synchronize()
-    T = 12
+    T = int(sys.argv[2]) if len(sys.argv) > 2 else (12 if os.environ["FA_FWD_VARIANT"] == "2401" else 10)
     t = q[-1].reshape(-1).view(torch.int64)[: 4 * T * 4 * 2].cpu().numpy().reshape(4 * T, 4, 2).astype(np.int64)
     for g in range(2):
         ts = t[:, :, g]
