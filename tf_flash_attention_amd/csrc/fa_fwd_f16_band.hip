@@ -82,8 +82,12 @@ constexpr int kBLead1 = 64;
 constexpr int kBStag = 128;
 constexpr int kMinTStag = 10;
 constexpr int kMaxTStag = 22;
-constexpr int kBandDefault = kBFPMax | kBStag;  // round 3: staggered groups
-constexpr int kBandR3 = kBFPMax;                // round 3 before the stagger: T positions for T tiles
+// the finished item's epilogue out of VALU(0): l / m and the new item's lane state at the tail of
+// MFMA(0); O into LDS there too for group 1, at the head of MFMA(1) for group 0 (each beside the
+// other group's first softmax, instead of stretching its own VALU(0))
+constexpr int kBEpiSplit = 256;
+constexpr int kBandDefault = kBFPMax | kBStag | kBEpiSplit;  // round 3: staggered groups, split epilogue
+constexpr int kBandR3 = kBFPMax;                             // round 3 before the stagger: T positions for T tiles
 
 // staggered staging schedule (T positions, NT = T + 2 tiles an item, rings of four slots: tile j in
 // slot j & 3).  Tile j of an item is read by group 0 as K at position j (j < T) and as V at j + 1, by
@@ -590,6 +594,50 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
 
   // O, l, m of the item that just finished (its last PV ran in the MFMA phase before) into LDS:
   // O [c][256 q] fp16 over the finished item's Q buffer, l / m at the l/m area
+  // (kBEpiSplit) the parts: l / m into LDS (returns 1/l), O into LDS
+  auto epi_lm = [&]() -> float __attribute__((always_inline)) {
+    const float l_tot = sum_pair32((lacc[0] + lacc[1]) + (lacc[2] + lacc[3]));
+    const float inv = (l_tot > 0.f) ? __builtin_amdgcn_rcpf(l_tot) : 0.f;
+    const float m_fin = PMAX ? max_pair32(fmaxf(m_max, m_run + __log2f((float)__builtin_elementwise_maximum(pmr[0], pmr[1]))))
+                             : m_max;
+    if (h == 0) {
+      float lv = 0.f;
+      __half mv = neg_inf_approx<__half>();
+      if (l_tot > 0.f) {
+        mv = __float2half(m_fin * kLn2);
+        lv = l_tot * __builtin_amdgcn_exp2f(m_run - __half2float(mv) * kLog2e);
+      }
+      *reinterpret_cast<__attribute__((address_space(3))) float*>(smem + kOffLM + 4 * (32 * w + r)) = lv;
+      *reinterpret_cast<__attribute__((address_space(3))) unsigned short*>(smem + kOffLM + 4 * kBM + 2 * (32 * w + r)) =
+          __half_as_ushort(mv);
+    }
+    return inv;
+  };
+  auto epi_o = [&](float inv) __attribute__((always_inline)) {
+    lds_char_t* ob = smem + ((n + 1) & 1) * kQImg + 2 * (32 * w + r);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int cch = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+        *reinterpret_cast<__attribute__((address_space(3))) _Float16*>(ob + cch * kQRow) = (_Float16)(o[u][i] * inv);
+        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+  };
+  float oinv = 0.f;  // (kBEpiSplit, group 0) the finished item's 1/l from MFMA(0) to MFMA(1)
+  auto item_switch = [&]() __attribute__((always_inline)) {
+    const float inv = epi_lm();
+    if (grp == 1) epi_o(inv);
+    else oinv = inv;
+    m_max = kNegInf;
+    if constexpr (!PMAX) thr = kMaskFloor;
+    m_run = 0.f;
+    if constexpr (PMAX) {
+      pmr = half2v{(_Float16)0.f, (_Float16)0.f};
+      thr_h = (_Float16)-1.f;
+    }
+    item_state(cur);
+  };
   auto epilogue_lds = [&]() __attribute__((always_inline)) {
     const float l_tot = sum_pair32((lacc[0] + lacc[1]) + (lacc[2] + lacc[3]));
     const float inv = (l_tot > 0.f) ? __builtin_amdgcn_rcpf(l_tot) : 0.f;
@@ -646,6 +694,12 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     // every fragment is read in the phase that uses it, two k-steps ahead (nothing lives across
     // the VALU phase: the register budget holds the stream's staging); the first two K k-steps
     // are read at the phase start, their latency the only one exposed
+    if constexpr ((F & kBEpiSplit) != 0 && it == 1) {  // group 0: the finished item's O, before o restarts
+      if (grp == 0 && n > 0) {
+        epi_o(oinv);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     half8 kf[4][2], vf[4][2];
     read_kstep(pk, 0, kf[0]);
     read_kstep(pk, 1, kf[1]);
@@ -756,6 +810,13 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       if constexpr (it + kA - 1 < T) vst[x] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (it + kA - 1) * kBN);
       else vst[x] = load(vrs, voff, nxt.sl * vsl, nxt.kt0 + (it + kA - 1 - T) * kBN);
     }
+    if constexpr ((F & kBEpiSplit) != 0 && it == 0) {
+      // the finished item's l / m (and group 1's O: its last PV ran above); the new item's state
+      if (n > 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        item_switch();
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -764,7 +825,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   auto valu_phase = [&](auto IT_) __attribute__((always_inline)) {
     constexpr int it = decltype(IT_)::value;
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's staging stores / reads landed
-    if constexpr (it == 0) {
+    if constexpr (it == 0 && (F & kBEpiSplit) == 0) {
       if (n > 0) {
         epilogue_lds();
         __builtin_amdgcn_sched_barrier(0);  // the epilogue's temporaries die before the softmax's
@@ -951,7 +1012,7 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
 #ifdef FA_DIAG
   // FA_FWD_VARIANT: 2400 the unstaggered structure (T positions for T tiles), 2401 its stamp build,
   // 2402 either with the contiguous item order, 2403-2410 its ablations / A-B (T = 12 only), 2421
-  // the staggered stamp build (T' = 10)
+  // the default's stamp build (T' = 10), 2422 the staggered kernel with the whole epilogue in VALU(0)
   const int dv = diag_variant("FA_FWD_VARIANT");
   if (dv == 2402) ba.inter = 0;  // round-2 order: contiguous runs of items
   if (dv >= 2400 && dv < 2420 && dv != 2402) {
@@ -976,6 +1037,7 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
     }
   }
   if (dv == 2421 && ba.T == 10) return launch_band_t<10, true>(ba, s);
+  if (dv == 2422 && ba.T == 10) return launch_band_t<10, false, kBFPMax | kBStag>(ba, s);  // epilogue in VALU(0)
 #endif
   switch (ba.T) {
     case 10: return launch_band_t<10>(ba, s);

@@ -1,6 +1,7 @@
-"""Bitwise A/B of the persistent band forward against a diagnostic variant (default: 2420, the
-staggered groups) over a set of 1d local-window shapes the band kernel takes (diagnostic library).
-A variant that keeps every wave's tile sequence must give the same O, l, m bits.
+"""Bitwise A/B of the persistent band forward (the default: staggered groups, split epilogue)
+against a diagnostic variant (default: 2400, the unstaggered structure) over a set of 1d
+local-window shapes the band kernel takes (diagnostic library).  A variant that keeps every wave's
+tile sequence must give the same O, l, m bits.
 Usage: python tools/band_stag_check.py [variant]"""
 import json
 import os
@@ -28,7 +29,7 @@ SHAPES = [
 
 
 def main():
-    variant = sys.argv[1] if len(sys.argv) > 1 else "2420"
+    variant = sys.argv[1] if len(sys.argv) > 1 else "2400"
     dev = torch.device("cuda:0")
     worst = 0.0
     for (b, d, nq, nk, sync, ws, la) in SHAPES:
