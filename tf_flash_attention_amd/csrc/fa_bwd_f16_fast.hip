@@ -1323,443 +1323,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
     return acc;
   };
   const int qo = (POL == 2) ? seq_order(a.rule.q, a.rule, min(qi, nq - 1)) : 0;  // this lane's query order
-
-  // ---- key-tile staging (K, V chunks: 8 keys of one channel row)
-  uint32_t voff[kCPT];
-  int crow_[kCPT];
-  const int cm = tid & 7;
-#pragma unroll
-  for (int j = 0; j < kCPT; ++j) {
-    crow_[j] = ((tid + kThr * j) % kKChunks) >> 3;
-    voff[j] = (uint32_t)crow_[j] * (uint32_t)nk * 2u + (ALN ? 16u * cm : 0u);  // (ALN: the chunk's; else the row's)
-  }
-  // two staging sets (tile t in set t&1): a tile is loaded two steps before it is stored
-  u32x4 kr[2][kCPT];
-  auto is_v = [&](int j) -> bool {
-    return (kKChunks % kThr == 0) ? (j >= kKChunks / kThr) : ((tid + kThr * j) >= kKChunks);
-  };
-  auto load_tile = [&](int ka, int set) {
-    const bool out = ka + 8 * cm >= nk;
-#pragma unroll
-    for (int j = 0; j < kCPT; ++j) {
-      const bool isV = is_v(j);
-      if constexpr (ALN)
-        kr[set][j] = buf_load16(isV ? vrs : krs, voff[j], 2 * min(ka, nk), out || crow_[j] >= (isV ? vd : d));
-      else
-        kr[set][j] = buf_load8h(isV ? vrs : krs, voff[j], ka + 8 * cm, nk, crow_[j] < (isV ? vd : d));
-    }
-  };
-  auto store_tile = [&](int slot, int set) {
-    lds_char_t* base = smem + slot * S::kSlot;
-#pragma unroll
-    for (int j = 0; j < kCPT; ++j) {
-      const bool isV = is_v(j);
-      *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[set][j];
-    }
-  };
-  floatx16 dq[D / 32];
-#pragma unroll
-  for (int u = 0; u < D / 32; ++u)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dq[u][i] = 0.f;
-
-  // A-operand (Kᵀ / Vᵀ) read bases: lane 4q+p of a 16-lane group supplies channel row q, keys
-  // 4σ(p)..4σ(p)+3 (σ swaps 1 and 2), so register i of Sᵀ / dPᵀ half t holds key 32t + 16(i>>3) +
-  // 8h + (i&7): k-step s of dSᵀ is keys 16s + 8h + 0..7 and K's dQ A operand is one b128 row read
-  const int sig = ((tp & 1) << 1) | (tp >> 1);
-  uint32_t tb[2][2];  // [e][t], row 8(g>>1) + 4e + tq (+16s: immediate)
-#pragma unroll
-  for (int e = 0; e < 2; ++e)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) tb[e][t] = k2_off(8 * (g >> 1) + 4 * e + tq, 4 * t + 2 * (g & 1) + (sig >> 1), sig & 1);
-  uint32_t kb2[4];  // dQ A operand: row 32u + r (+32u·128: immediate), chunk 2s + h
-#pragma unroll
-  for (int s = 0; s < 4; ++s) kb2[s] = k2_off(r, 2 * s + h);
-
-  // unconditional (with no tiles it moves zeros): a conditional load here left hipcc's vmcnt
-  // state merged, and the loop's first step then drained every load in flight
-  load_tile(kt0, 0);
-  store_tile(0, 0);
-  load_tile(kt0 + kBN, 1);
-  load_tile(kt0 + 2 * kBN, 0);
-
-  auto step = [&](auto P_, int it) {
-    constexpr int p = decltype(P_)::value;
-    __syncthreads();
-    const int ka = kt0 + it * kBN;
-    const int cls = it < ntiles ? tcls(ka) : 0;  // (the loop's last pair may end on a phantom step)
-    // unconditional (past the end they move zeros into a slot nobody reads): exact vmcnt waits
-    store_tile(p ^ 1, p ^ 1);
-    load_tile(ka + 3 * kBN, p ^ 1);
-    if (cls == 0) return;
-    const lds_char_t* base = smem + p * S::kSlot;
-    floatx16 st[2], dp[2];
-    // PRE: every operand read two MFMA pairs ahead of its MFMAs (one wave per SIMD: nothing else
-    // hides an LDS round trip between a read and the MFMA that consumes it)
-    half8 ka8p[3];
-    auto rka = [&](int n) __attribute__((always_inline)) {  // dQ operand n = 4s + u
-      ka8p[n % 3] = read_b128(base + S::offKT + kb2[n / (D / 32)] + 32 * (n % (D / 32)) * 128);
-    };
-    if constexpr (PRE) {
-      constexpr int kN = 2 * (D / 16);
-      half8 kf[3], vf[3];
-      auto rd = [&](int n) __attribute__((always_inline)) {  // n = 2s + t
-        const int s_ = n >> 1, t = n & 1;
-        const uint32_t b0 = tb[0][t] + (16 * s_) * 128, b1 = tb[1][t] + (16 * s_) * 128;
-        kf[n % 3].lo = tr_read(base + S::offKT + b0);
-        kf[n % 3].hi = tr_read(base + S::offKT + b1);
-        vf[n % 3].lo = tr_read(base + S::offVT + b0);
-        vf[n % 3].hi = tr_read(base + S::offVT + b1);
-      };
-      rd(0);
-      rd(1);
-#pragma unroll
-      for (int n = 0; n < kN; ++n) {
-        if (n + 2 < kN) rd(n + 2);
-        if (n == kN - 2) rka(0);
-        if (n == kN - 1) rka(1);
-        const int s_ = n >> 1, t = n & 1;
-        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[n % 3], qf[s_], s_ == 0 ? negl : st[t], 0, 0, 0);
-        dp[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[n % 3], of[s_], s_ == 0 ? negd : dp[t], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < (PRE ? 0 : D / 16); ++s)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        half8 kf, vf;
-        const uint32_t b0 = tb[0][t] + (16 * s) * 128, b1 = tb[1][t] + (16 * s) * 128;
-        kf.lo = tr_read(base + S::offKT + b0);
-        kf.hi = tr_read(base + S::offKT + b1);
-        vf.lo = tr_read(base + S::offVT + b0);
-        vf.hi = tr_read(base + S::offVT + b1);
-        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], s == 0 ? negl : st[t], 0, 0, 0);
-        dp[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, of[s], s == 0 ? negd : dp[t], 0, 0, 0);
-      }
-    // dSᵀ = exp2(Sᵀ)∘dPᵀ; keys of register i of half t: 32t + 16(i>>3) + 8h + (i&7)
-    auto dsq = [&](int cl) __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      half8 dsf;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int t = s >> 1, i = 8 * (s & 1) + j;
-        float pv = __builtin_amdgcn_exp2f(st[t][i]);
-        if (cl == 1) {
-          const int kk = ka + 32 * t + 16 * (i >> 3) + 8 * h + (i & 7);
-          const bool ok = (POL == 1)   ? ((unsigned)(kk - klo) < (unsigned)kspan)
-                          : (POL == 2) ? (kk < nk && check_orders_bf(a.rule, qo, seq_order(a.rule.k, a.rule, min(kk, nk - 1))))
-                                       : (kk < nk);
-          pv = ok ? pv : 0.f;
-        }
-        dsf[j] = (_Float16)(pv * dp[t][i]);
-      }
-#pragma unroll
-      for (int u = 0; u < D / 32; ++u) {
-        if constexpr (PRE) {
-          const int n = (D / 32) * s + u;
-          if (n + 2 < 4 * (D / 32)) rka(n + 2);
-          dq[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka8p[n % 3], dsf, dq[u], 0, 0, 0);
-        } else {
-          const half8 ka8 = read_b128(base + S::offKT + kb2[s] + 32 * u * 128);
-          dq[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka8, dsf, dq[u], 0, 0, 0);
-        }
-      }
-    }
-    };
-    // the edge-tile mask as a real branch (see the producer / consumer pass; MSPEC: the if-converted form)
-    if constexpr (MSPEC) {
-      dsq(cls);
-    } else if (cls == 1) {
-      asm volatile("; edge tile" ::: );
-      dsq(1);
-    } else {
-      asm volatile("; interior tile" ::: );
-      dsq(2);
-    }
-  };
-  for (int it = 0; it < ntiles; it += 2) {  // whole pairs (see the dK/dV pass)
-    step(IC<0>{}, it);
-    step(IC<1>{}, it + 1);
-  }
-
-  if (!wave_active || qi >= nq) return;
-  __half* dQ = static_cast<__half*>(a.dQ) + bi * (int64_t)d * nq;
-  const float sc = (float)a.scale;
-  if (d == D) {  // one buffer store per value (see the dK/dV pass)
-    const __amdgpu_buffer_rsrc_t qrs_ = make_rsrc(dQ, 2u * d * nq);
-    const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nq + (uint32_t)qi);
-#pragma unroll
-    for (int u = 0; u < D / 32; ++u)
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(dq[u][i] * sc)), qrs_, vlane,
-                                              2u * (32u * u + (i & 3) + 8u * (i >> 2)) * (uint32_t)nq, 0);
-    return;
-  }
-#pragma unroll
-  for (int u = 0; u < D / 32; ++u)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-      if (c < d) dQ[(int64_t)c * nq + qi] = __float2half(dq[u][i] * sc);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// dQ, producer / consumer (two waves per SIMD): the dK/dV pass's split applied to the query-outer
-// pass.  Waves w and w+4 share a SIMD and the same 32 queries.  Wave w (producer) keeps Q' and dO
-// resident, forms Sᵀ = Kᵀ·Q' and dPᵀ = Vᵀ·dO for key tile i one 32-key half at a time and
-// dSᵀ = exp2(Sᵀ)∘dPᵀ, and hands dSᵀ to wave w+4 through LDS (four lane-linear b128 per lane);
-// wave w+4 (consumer) stages the key tiles and accumulates dQ += K·dSᵀ for tile i-1.  The
-// one-wave-per-SIMD pass above (332-345 registers) serialises its softmax and every LDS round trip
-// behind its own MFMAs; here the producer's softmax runs beside the consumer's MFMAs and staging.
-// Ring: four K/V slots (tile t in slot t % 4), two hand-over slots, one barrier per step;
-// 4 x 32 KB + 32 KB = 160 KB at D = 128.
-template <int D>
-struct DqPcSmem {
-  static constexpr int kBM = 128;           // queries per workgroup: four producer waves x 32
-  static constexpr int kRow = D * kBM * 2;  // Q (or dO) row image (prologue only)
-  static constexpr int kKT = D * 128;       // one [D][64] K2 image
-  static constexpr int offKT = 0, offVT = kKT;
-  static constexpr int kSlot = 2 * kKT;
-  static constexpr int kNS = 4;
-  static constexpr int offX = kNS * kSlot;  // dSᵀ hand-over: 2 slots x 4 waves x 4 KB
-  static constexpr int kXWave = 4096, kXSlot = 4 * kXWave;
-  static constexpr int kUsed = offX + 2 * kXSlot;
-  static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;  // the Q/dO images alias the ring
-};
-
-template <int D, int POL, bool ALN, int PF = 0>
-__global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  lds_char_t* smem = (lds_char_t*)smem_raw;
-  using S = DqPcSmem<D>;
-  // PF & 4 (diagnostic build): per-wave s_memtime sums of each step's parts, written to the unused
-  // dQ workspace (producer: barrier, half-0 MFMAs, half-0 softmax, half-1 MFMAs, half-1 softmax;
-  // consumer: barrier, staging, hand-over reads, MFMAs)
-  constexpr bool STAMP = (PF & 4) != 0;
-  uint64_t stv[5] = {0, 0, 0, 0, 0}, st_prev = 0;
-  auto stamp = [&](int k) __attribute__((always_inline)) {
-    if constexpr (STAMP) {
-      __builtin_amdgcn_sched_barrier(0);
-      uint64_t t;
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      if (k >= 0) stv[k] += t - st_prev;
-      st_prev = t;
-    }
-  };
-  constexpr int kThr = 512, kHalfThr = 256;  // one half of the workgroup stages
-  constexpr int kBM = S::kBM, kBN = 64;
-  constexpr int kKChunks = D * 8;  // 16-B chunks of one [D][64] tile
-  static_assert((2 * kKChunks) % kHalfThr == 0, "tile chunks must divide over the staging waves");
-  constexpr int kCPT = 2 * kKChunks / kHalfThr;  // K and V chunks per staging thread
-  constexpr float kNegInf = -__builtin_huge_valf();
-
-  const int nq = a.rule.q.n, nk = a.rule.k.n;
-  const uint32_t nqb = (nq + kBM - 1) / kBM;
-  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t bi = bid / nqb;
-  const int q0 = (int)(nqb - 1 - (bid % nqb)) * kBM;  // latest (heaviest under causal) blocks first
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = w >> 2, wl = w & 3;  // group 0 produces, group 1 consumes; wl: the query slice
-  const int h = lane >> 5, r = lane & 31;
-  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
-  const float c2 = (float)a.scale * kLog2e;
-  auto stamp_out = [&]() __attribute__((always_inline)) {
-    if constexpr (STAMP) {
-      if (lane < 5) {
-        uint64_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) v = (lane == k) ? stv[k] : v;
-        reinterpret_cast<uint64_t*>(a.ws_dQ)[((int64_t)bid * 8 + w) * 8 + lane] = v;
-      }
-    }
-  };
-
-  const int d = a.d, vd = a.v_d;
-  const __half* Q = static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq;
-  const __half* dO = static_cast<const __half*>(a.dO) + bi * (int64_t)vd * nq;
-
-  const int wq0 = q0 + 32 * wl;
-  const int qi = wq0 + r;
-  const bool wave_active = wq0 < nq;
-
-  // ---- Q, dO blocks into LDS (every thread); the producers read their resident B operands below
-  {
-    constexpr int kRPT = 2 * D * (kBM / 8) / kThr, kHalf = D * (kBM / 8) / kThr;
-    static_assert(kHalf * kThr == D * (kBM / 8), "resident chunks must divide over the workgroup");
-    const __amdgpu_buffer_rsrc_t qrs2 = make_rsrc(Q, 2u * d * nq), ors2 = make_rsrc(dO, 2u * vd * nq);
-    u32x4 rv[kRPT];
-#pragma unroll
-    for (int jj = 0; jj < kRPT; ++jj) {
-      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
-      const int c = j / (kBM / 8), m = j % (kBM / 8);
-      const bool in = c < (which ? vd : d) && q0 + 8 * m < nq;
-      if constexpr (ALN)
-        rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? ors2 : qrs2,
-                                                       in ? (uint32_t)c * (uint32_t)nq * 2u + 16u * m : 0x80000000u, 2 * q0, 0);
-      else
-        rv[jj] = buf_load8h(which ? ors2 : qrs2, (uint32_t)c * (uint32_t)nq * 2u, q0 + 8 * m, nq, c < (which ? vd : d));
-    }
-#pragma unroll
-    for (int jj = 0; jj < kRPT; ++jj) {
-      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
-      const int c = j / (kBM / 8), m = j % (kBM / 8);
-      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBM) + ((m * 16) ^ ((c & 3) << 6))) = rv[jj];
-    }
-  }
-  __syncthreads();
-
-  // ---- key range of this query block (rule-bounded), per-lane / per-wave key intervals (both roles)
-  const int qlast = min(q0 + kBM, nq) - 1;
-  int kb = 0, ke = nk;
-  if (POL != 0) k_range_for_q_block(a.rule, q0, qlast, &kb, &ke);
-  const int kt0 = (kb / kBN) * kBN;
-  const int ntiles = (ke > kb) ? (ke - kt0 + kBN - 1) / kBN : 0;
-  int klo = 0, kspan = nk, wlo_min = 0, wlo_max = 0, whi_min = nk - 1, whi_max = nk - 1;
-  if (POL == 1 && wave_active) {
-    int khi;
-    key_interval(a.rule, min(qi, nq - 1), &klo, &khi);
-    kspan = max(khi - klo + 1, 0);
-    const int last = min(31, nq - 1 - wq0);
-    wlo_min = __builtin_amdgcn_readfirstlane(klo);
-    whi_min = __builtin_amdgcn_readfirstlane(khi);
-    wlo_max = __builtin_amdgcn_readlane(klo, last);
-    whi_max = __builtin_amdgcn_readlane(khi, last);
-  }
-  auto tcls = [&](int ka) -> int {
-    const int kz = ka + kBN - 1;
-    if (!wave_active) return 0;
-    if (POL == 0) return kz < nk ? 2 : 1;
-    if (POL == 2) {  // class 2 only for tiles wholly inside nk (the staged tail past nk is masked)
-      if (ka >= nk) return 0;
-      const int c = tile_class(a.rule, wq0, min(wq0 + 31, nq - 1), ka, min(kz, nk - 1));
-      return (c == 2 && kz >= nk) ? 1 : c;
-    }
-    if (wlo_min > kz || whi_max < ka) return 0;
-    return (wlo_max <= ka && whi_min >= kz && kz < nk) ? 2 : 1;
-  };
-  // hand-over slot of this wave pair: k-steps 0..3 of dSᵀ, one b128 each, lane-linear
-  auto xoff = [&](int xs, int j) -> uint32_t { return S::offX + xs * S::kXSlot + wl * S::kXWave + j * 1024 + lane * 16; };
-  // Steps it = 0 .. ntiles: the producer handles tile it (it < ntiles), the consumer tile it-1 (it >= 1),
-  // in whole groups of four (ring slot it % 4, staging set (it+1) % 2, hand-over slot it % 2 compile-time)
-  const int nsteps = ntiles + 1;
-
-  // ---- key-tile staging (K, V chunks: 8 keys of one channel row) by the consumer half of the workgroup
-  const int ct = tid & (kHalfThr - 1);
-  const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + bi * (int64_t)d * nk, 2u * d * nk);
-  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk, 2u * vd * nk);
-  uint32_t voff[kCPT];
-  int crow_[kCPT];
-  const int cm = ct & 7;
-#pragma unroll
-  for (int j = 0; j < kCPT; ++j) {
-    crow_[j] = ((ct + kHalfThr * j) % kKChunks) >> 3;
-    voff[j] = (uint32_t)crow_[j] * (uint32_t)nk * 2u + (ALN ? 16u * cm : 0u);
-  }
-  u32x4 kr[2][kCPT];  // two staging sets: tile t in set t&1, loaded two steps before it is stored
-  auto is_v = [&](int j) -> bool {
-    return (kKChunks % kHalfThr == 0) ? (j >= kKChunks / kHalfThr) : ((ct + kHalfThr * j) >= kKChunks);
-  };
-  auto load_tile = [&](int ka, int set) __attribute__((always_inline)) {
-    const bool out = ka + 8 * cm >= nk;
-#pragma unroll
-    for (int j = 0; j < kCPT; ++j) {
-      const bool isV = is_v(j);
-      if constexpr (ALN)
-        kr[set][j] = buf_load16(isV ? vrs : krs, voff[j], 2 * min(ka, nk), out || crow_[j] >= (isV ? vd : d));
-      else
-        kr[set][j] = buf_load8h(isV ? vrs : krs, voff[j], ka + 8 * cm, nk, crow_[j] < (isV ? vd : d));
-    }
-  };
-  auto store_tile = [&](int slot, int set) __attribute__((always_inline)) {
-    lds_char_t* base = smem + slot * S::kSlot;
-#pragma unroll
-    for (int j = 0; j < kCPT; ++j) {
-      const bool isV = is_v(j);
-      *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[set][j];
-    }
-  };
-  // first tiles (after tile 0's loads): the barrier that retires the Q / dO images, tile 0 stored
-  auto stage0 = [&]() __attribute__((always_inline)) {
-    __syncthreads();
-    store_tile(0, 0);
-    load_tile(kt0 + kBN, 1);
-    load_tile(kt0 + 2 * kBN, 0);
-  };
-  // resident B operands of the producer, lane (r,h) holds X[c = 16s + 8h + j][q = wq0 + r]: Q' and dO;
-  // the row constants likewise
-  auto resident = [&](int img, half8* x) __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int crow = 16 * s + 8 * (g >> 1) + 4 * e + tq;
-        const int col = 32 * wl + 16 * (g & 1) + 4 * tp;
-        const uint32_t off = crow * (2 * kBM) + ((col * 2) ^ ((crow & 3) << 6));
-        const half4 v = tr_read(smem + img * S::kRow + off);
-        if (e == 0) x[s].lo = v; else x[s].hi = v;
-      }
-  };
-  auto rowconst = [&](const void* ws, float dflt) -> floatx16 {
-    const float* p = static_cast<const float*>(ws) + bi * (int64_t)nq;
-    const float v = (qi < nq) ? p[qi] : dflt;
-    floatx16 x;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = v;
-    return x;
-  };
-  // A-operand (Kᵀ / Vᵀ) read bases, σ-permuted as in the one-wave pass: register i of half t holds
-  // key 32t + 16(i>>3) + 8h + (i&7), so k-step s of dSᵀ is keys 16s + 8h + 0..7
-  const int sig = ((tp & 1) << 1) | (tp >> 1);
-  uint32_t tb[2][2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) tb[e][t] = k2_off(8 * (g >> 1) + 4 * e + tq, 4 * t + 2 * (g & 1) + (sig >> 1), sig & 1);
-  // Sᵀ (or dPᵀ) of key half t: 8 MFMAs over the channels, transposed A reads two k-steps ahead
-  auto half_chain = [&](const lds_char_t* img, const half8* bres, floatx16 init, int t) __attribute__((always_inline)) -> floatx16 {
-    constexpr int kS = D / 16;
-    half8 af[3];
-    auto rd = [&](int s_) __attribute__((always_inline)) {
-      af[s_ % 3].lo = tr_read(img + tb[0][t] + (16 * s_) * 128);
-      af[s_ % 3].hi = tr_read(img + tb[1][t] + (16 * s_) * 128);
-    };
-    rd(0);
-    rd(1);
-    floatx16 acc = init;
-#pragma unroll
-    for (int s_ = 0; s_ < kS; ++s_) {
-      if (s_ + 2 < kS) rd(s_ + 2);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s_ % 3], bres[s_], acc, 0, 0, 0);
-    }
-    return acc;
-  };
-  // (PF & 16) Sᵀ and dPᵀ of key half t as two interleaved chains: k-step s of both issues back to back,
-  // the K and V fragment reads of k-step s+2 after them (twice the MFMA cover per read)
-  auto dual_chain = [&](const lds_char_t* base, const half8* q_, const half8* o_, floatx16& st, floatx16& dp, int t)
-                        __attribute__((always_inline)) {
-    constexpr int kS = D / 16;
-    half8 kf[3], vf[3];
-    auto rd = [&](int s_) __attribute__((always_inline)) {
-      kf[s_ % 3].lo = tr_read(base + S::offKT + tb[0][t] + (16 * s_) * 128);
-      kf[s_ % 3].hi = tr_read(base + S::offKT + tb[1][t] + (16 * s_) * 128);
-      vf[s_ % 3].lo = tr_read(base + S::offVT + tb[0][t] + (16 * s_) * 128);
-      vf[s_ % 3].hi = tr_read(base + S::offVT + tb[1][t] + (16 * s_) * 128);
-    };
-    rd(0);
-    rd(1);
-#pragma unroll
-    for (int s_ = 0; s_ < kS; ++s_) {
-      st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[s_ % 3], q_[s_], st, 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s_ % 3], o_[s_], dp, 0, 0, 0);
-      if (s_ + 2 < kS) rd(s_ + 2);
-    }
-  };
-  const int qo = (POL == 2) ? seq_order(a.rule.q, a.rule, min(qi, nq - 1)) : 0;  // this lane's query order
   // P of register i of key half t (exp2 of the score, zero outside the rule)
   auto pval = [&](float sv, int cls, int ka, int t, int i) __attribute__((always_inline)) -> float {
     float pv = __builtin_amdgcn_exp2f(sv);
