@@ -24,6 +24,9 @@ SHAPES = [
     (5, 64, 800, 800, "scale_end", 511, False),
     (2, 64, 4096, 4096, "none_front", 600, False),
     (2, 64, 264, 264, "none_front", 16, False),
+    (2, 64, 3000, 3000, "none_front", 300, False),
+    (1, 64, 200, 200, "none_front", 50, True),
+    (3, 40, 1024, 2048, "scale_front", 128, True),
     (64, 64, 16384, 16384, "none_front", 256, False),
 ]
 
