@@ -4,7 +4,8 @@
 Default (the driver's contract): BASELINE.json config 2 — full_1d fp16,
 B=8 H=16 d=64 Nq=Nk=4096, forward — metric "fwd TFLOP/s per GPU + MFMA util %".
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--shard|--weak]
+                  [--no-cpu-baseline]
 
 For N>1: one process per GPU, each rank runs its own shard of batch×head
 slices (no data-path collective; a gloo barrier / max-reduce over CPU tensors
@@ -12,9 +13,11 @@ only brackets the timed region).  Under torch.distributed.run the ranks come
 from the environment; without it (WORLD_SIZE unset) `--gpus N` starts N fresh
 child processes itself, before anything touches the GPU, and exits with the
 worst child's status.
-c2/c3/c5: every rank processes the full config batch (weak scaling);
-c4: the config's b=1024 slices are split across ranks (strong scaling, as the
-config prescribes "batch-sharded across 8×MI355X").
+Default (--shard): the config's batch×head slices are split across the ranks
+(strong scaling: c2 b=128 is 64 slices a rank at N=2, 16 at N=8), so a 1→8
+curve measures the op's batch-shard efficiency (BASELINE north_star: "near-linear
+batch-shard scaling").  --weak: every rank runs the whole config batch (the
+round-1..3 behaviour for c2/c3/c5).
 
 A step = one pass of the op over the rank's batch with inputs resident in HBM
 (c3: forward + backward).  Prints ONE JSON line on rank 0.
@@ -42,7 +45,7 @@ MFMA_PEAK = {"fp16": 2516.6, "fp32": 157.3, "fp64": 78.6}   # dense TFLOP/s (MI3
 HBM_PEAK_GBS = 8000.0
 
 CONFIGS = {
-    # name: (policy, seq_dims, dtype, batch, d, q_seq, k_seq, sync, ws, ls, causal, backward, scaling)
+    # name: (policy, seq_dims, dtype, batch, d, q_seq, k_seq, sync, ws, ls, causal, backward, -)
     "c2": ("full", 1, torch.float16, (8, 16), 64, (4096,), (4096,), "none_front", 1, 0, False, False, "weak"),
     "c3": ("causal", 1, torch.float16, (8, 16), 128, (8192,), (8192,), "none_front", 1, 0, False, True, "weak"),
     "c4": ("local", 1, torch.float16, (64, 16), 64, (16384,), (16384,), "none_front", 256, 0, False, False, "strong"),
@@ -59,6 +62,16 @@ WORKLOAD = {
     "d32": "full_1d fp16 B=8 H=16 d=32 Nq=Nk=4096 forward (config 2 at the reference tests' d=32; diagnostic)",
 }
 DTYPE_NAME = {torch.float16: "fp16", torch.float32: "fp32", torch.float64: "fp64"}
+
+
+def rank_batch(cfg, world: int, rank: int, weak: bool = False):
+    """(slices this rank runs, "strong"|"weak"): by default the config's flattened batch split into
+    contiguous slabs (shard.shard_range); with ``weak`` every rank runs all of it."""
+    b_total = int(np.prod(cfg[3]))
+    if weak:
+        return b_total, "weak"
+    s0, s1 = shard.shard_range(b_total, world, rank)
+    return s1 - s0, "strong"
 
 
 def _call_forward(cfg, q, k, v):
@@ -223,6 +236,10 @@ def main():
     # W steps until this much wall time has gone by; the line reports both
     ap.add_argument("--warmup-s", type=float, default=1.0)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--shard", dest="weak", action="store_false", default=False,
+                    help="split the config's batch across ranks (strong scaling; the default)")
+    ap.add_argument("--weak", dest="weak", action="store_true",
+                    help="every rank runs the whole config batch (weak scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     args = ap.parse_args()
@@ -254,13 +271,9 @@ def main():
     dev = torch.device("cuda", local % ndev)
 
     cfg = CONFIGS[args.config]
-    policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, scaling = cfg
-    b_total = int(np.prod(batch))
-    if scaling == "strong":  # the config's slices split across ranks (contiguous slabs, no collective)
-        s0, s1 = shard.shard_range(b_total, world, rank)
-        b_rank = s1 - s0
-    else:                    # every rank runs the full config batch
-        b_rank = b_total
+    policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, _ = cfg
+    # the config's slices split across ranks (contiguous slabs, no collective), or all of them
+    b_rank, scaling = rank_batch(cfg, world, rank, args.weak)
     shape_q = (b_rank, d) + qs
     shape_k = (b_rank, d) + ks
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -359,7 +372,8 @@ def main():
             "vs_baseline": None,
             "dtype": dname,
             "data": "synthetic U(-2,2), generated on device",
-            "config": {"workload": WORKLOAD[args.config], "b_per_rank": b_rank, "d": d, "q_seq": list(qs),
+            "config": {"workload": WORKLOAD[args.config], "b_total": int(np.prod(batch)) * (world if args.weak else 1),
+                       "b_per_rank": b_rank, "d": d, "q_seq": list(qs),
                        "k_seq": list(ks), "policy": policy, "sync_mode": sync,
                        "parallelism": f"batch-shard x{world} (no collective)"},
             "per_gpu_tflops": round(value / world, 3),

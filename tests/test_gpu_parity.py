@@ -403,10 +403,10 @@ def diag_lib(monkeypatch):
     from tf_flash_attention_amd import _lib
     if not __import__("os").path.exists(_lib.DIAG_LIB_PATH):
         pytest.skip("libfa_hip_diag.so not built (make -C tf_flash_attention_amd diag)")
-    with _lib.using(_lib.DIAG_LIB_PATH):
+    with _lib.using(_lib.DIAG_LIB_PATH) as h:
         info = _lib.build_info()
         assert "lib=diag" in info and f"src={_lib.source_hash(diag=True)};" in info, info
-        yield
+        yield h
 
 
 VARIANT_CASES = [
@@ -449,5 +449,11 @@ def test_f16_forward_structures_d128(monkeypatch, diag_lib, variant, policy, seq
 @pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, True)])
 def test_f16_backward_read_placement(monkeypatch, diag_lib, variant, d, policy, ws, causal):
     monkeypatch.setenv("FA_BWD_VARIANT", variant)
+    # autograd runs the backward on its own device thread: the diagnostic library must still be
+    # the one that launches it (its call counter moves; the product library has none)
+    calls = diag_lib.fa_diag_call_count
+    calls.restype = __import__("ctypes").c_longlong
+    before = calls(1)
     run_case(np.float16, policy, 1, "none_front", (2,), d, d, (328,), (264,), ws=ws, ls=0, causal=causal,
              seed=int(variant) + d)
+    assert calls(1) == before + 1

@@ -89,3 +89,19 @@ def test_gloo_world2_shards_are_independent():
         covered += list(range(start, stop))
         assert tmax == [2.0, 10.0]
     assert covered == list(range(6))
+
+
+def test_bench_batch_shard_split():
+    """bench.py's default (--shard) splits every config's batch×head slices across the ranks, so
+    a 1→8 scaling run measures the op's shard efficiency; --weak keeps the whole batch per rank."""
+    import bench
+    for name, cfg in bench.CONFIGS.items():
+        b_total = int(np.prod(cfg[3]))
+        for world in (1, 2, 4, 8):
+            per = [bench.rank_batch(cfg, world, r) for r in range(world)]
+            assert sum(b for b, _ in per) == b_total, name
+            assert all(mode == "strong" for _, mode in per)
+            assert max(b for b, _ in per) - min(b for b, _ in per) <= 1
+            assert bench.rank_batch(cfg, world, 0, weak=True) == (b_total, "weak")
+    assert bench.rank_batch(bench.CONFIGS["c2"], 2, 1) == (64, "strong")
+    assert bench.rank_batch(bench.CONFIGS["c4"], 8, 7) == (128, "strong")

@@ -65,6 +65,10 @@ class FaProblem(ctypes.Structure):
 _lock = threading.Lock()
 _lib = None
 _tls = threading.local()  # .override: a library routed in by using() on THIS thread (tests: the diag build)
+# the library routed in by using() for the whole process: autograd runs a CUDA tensor's backward on
+# its own device thread, which does not see the thread-local override of the thread that called
+# .backward() (the diag-variant backward tests otherwise ran the product library)
+_process_override = None
 _loaded = {}
 DIAG_LIB_PATH = os.path.join(_HERE, "libfa_hip_diag.so")
 
@@ -106,6 +110,8 @@ def lib():
     ov = getattr(_tls, "override", None)
     if ov is not None:
         return ov
+    if _process_override is not None:
+        return _process_override
     if _lib is not None:
         return _lib
     with _lock:
@@ -128,7 +134,10 @@ def using(path):
     The GPU tests use it to run the diagnostic build (libfa_hip_diag.so, ``make -C
     tf_flash_attention_amd diag``): its FA_FWD_VARIANT / FA_BWD_VARIANT structures are not in
     the product library.  ctypes loads each library RTLD_LOCAL, so both can live in one process.
-    The routing is per thread: calls from other threads keep the product library."""
+    The routing covers this thread and, while the block runs, every other thread of the process
+    (autograd's device thread runs the backward of a CUDA tensor); blocks do not nest across
+    threads."""
+    global _process_override
     with _lock:
         h = _loaded.get(path)
         if h is None:
@@ -136,11 +145,14 @@ def using(path):
                 raise LibraryNotBuiltError(f"library not found at {path}")
             h = _loaded[path] = _declare(ctypes.CDLL(path))
     prev = getattr(_tls, "override", None)
+    prev_proc = _process_override
     _tls.override = h
+    _process_override = h
     try:
         yield h
     finally:
         _tls.override = prev
+        _process_override = prev_proc
 
 
 def make_problem(dtype, policy, seq_dims, sync_mode, b, q_seq, k_seq, d, v_d,

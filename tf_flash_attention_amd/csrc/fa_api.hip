@@ -70,8 +70,14 @@ int device_cus() {
   return cus;
 }
 
+// XCDs the block-placement maps assume (blocks dealt round-robin over them, 32 CUs each on gfx950).
+// The count is inferred from the CUs, exact only for parts built from 32-CU XCDs; any other CU count
+// returns 1, which turns the XCD-aware orders into plain ones (correct for every count: the maps are
+// bijections; only their L2-locality assumption needs the true count).
 int device_xcds() {
-  const int x = device_cus() / 32;
+  const int cus = device_cus();
+  if (cus % 32 != 0) return 1;
+  const int x = cus / 32;
   return x < 1 ? 1 : (x > 8 ? 8 : x);
 }
 
@@ -213,10 +219,20 @@ int fa_validate(const fa_problem* p) {
   return FA_OK;
 }
 
+#ifdef FA_DIAG
+// diagnostic library only: calls that reached a launch, so a test can prove which library ran them
+static std::atomic<long long> g_diag_calls[2];
+long long fa_diag_call_count(int which) { return (which == 0 || which == 1) ? g_diag_calls[which].load() : -1; }
+#define FA_DIAG_COUNT(w) g_diag_calls[w].fetch_add(1)
+#else
+#define FA_DIAG_COUNT(w) ((void)0)
+#endif
+
 int fa_forward(void* stream, const fa_problem* p, const void* Q, const void* K, const void* V, void* O, void* l,
                void* m) {
   int st = fa_validate(p);
   if (st != FA_OK) return st;
+  FA_DIAG_COUNT(0);
   fa::FwdArgs a;
   a.Q = Q; a.K = K; a.V = V; a.O = O; a.l = l; a.m = m;
   a.b = p->b; a.d = p->d; a.v_d = p->v_d;
@@ -254,6 +270,7 @@ int fa_backward(void* stream, const fa_problem* p, const void* Q, const void* K,
   const WsLayout w = ws_layout(p);
   if (workspace_bytes < w.total || (!workspace && w.total > 0))
     return set_error(FA_ERR_WORKSPACE_TOO_SMALL, "backward workspace is smaller than fa_backward_workspace_bytes()");
+  FA_DIAG_COUNT(1);
   fa::BwdArgs a;
   a.Q = Q; a.K = K; a.V = V; a.O = O; a.l = l; a.m = m; a.dO = dO;
   a.dQ = dQ; a.dK = dK; a.dV = dV;

@@ -124,9 +124,11 @@ __host__ __device__ constexpr int stag_v1(int T, int p, int g, int i) {
 __host__ __device__ constexpr int stag_nk(int T, int p) { return (p == 0 || p >= T - 2) ? 2 : 1; }
 __host__ __device__ constexpr int stag_nv(int T, int p) { return (p <= 1 || p == T - 1) ? 2 : 1; }
 constexpr float kRescaleThr = 8.f;
-// masked scores sit at or below -2^19 (the arithmetic edge mask); a row maximum at or below this
-// floor means "nothing allowed yet" (never a reference), and is the unset state of thr
-constexpr float kMaskFloor = -262144.f;
+// masked scores sit at or below -2^99 (the arithmetic edge mask); a row maximum at or below this
+// floor means "nothing allowed yet" (never a reference), and is the unset state of thr.  Every
+// finite score formed from fp16 inputs lies far inside (-2^98, 2^99), so no allowed score is clipped
+// and no disallowed one stays above an allowed one (the 2^20 scale had a +-2^18 range).
+constexpr float kMaskFloor = -0x1p98f;
 
 struct BandArgs {
   FwdArgs a;
@@ -438,15 +440,17 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   float lacc[4] = {0.f, 0.f, 0.f, 0.f};
 
   // edge-tile mask, arithmetic: key k0 + 8h + off is allowed iff 0 <= base + off < kspan (base = k0 +
-  // 8h - klo), so min(s, (base + off + 0.5)·2^20) (leading edge) and min(s, (kspan - base - off -
-  // 0.5)·2^20) (trailing edge) keep an allowed score (the bound is >= 2^19) and take a disallowed one
-  // to <= -2^19, whose exp2 is 0 against any reference.  One fma and one min per score and edge, no
+  // 8h - klo), so min(s, (base + off + 0.5)·2^100) (leading edge) and min(s, (kspan - base - off -
+  // 0.5)·2^100) (trailing edge) keep an allowed score (the bound is >= 2^99) and take a disallowed
+  // one to <= -2^99, whose exp2 is 0 against any reference (base + off + 0.5 is a half-integer of at
+  // most a few thousand, exact in fp32, and the power-of-two scale keeps it exact; past the fp32
+  // range the bound is +-inf with the same sign).  One fma and one min per score and edge, no
   // compare, no VCC select and so no hazard wait (the select form cost an add, a compare, a 2-state
   // s_nop and a v_cndmask per score); one copy of the code serves both edges (the edge picks the
   // per-lane constant and the sign), and a tile holding both edges (windows narrower than a tile)
   // runs it twice.  Rows with nothing allowed stay below kMaskFloor (never seeded).
   auto mask = [&](int k0, int cls) __attribute__((always_inline)) {
-    constexpr float kBig = 1048576.f;
+    constexpr float kBig = 0x1p100f;
     const float fb = (float)(k0 + 8 * h - klo);
     const float ca = __builtin_fmaf(fb, kBig, 0.5f * kBig), cb = __builtin_fmaf((float)kspan - fb, kBig, -0.5f * kBig);
     const int npass = cls == 1 ? 2 : 1;

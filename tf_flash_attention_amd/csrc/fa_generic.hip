@@ -608,6 +608,7 @@ hipError_t launch_fwd_generic_ch(const FwdArgs& a, hipStream_t stream) {
   const int64_t nqb = (a.rule.q.n + kGBQ - 1) / kGBQ;
   const int nvc = (a.v_d + kVC - 1) / kVC;
   const size_t smem = sizeof(A) * ((size_t)kDC * kGBQ + (size_t)kDC * kGBK + (size_t)kVC * kGBK + kGBQ * (kGBK + 1));
+  if (a.b * nqb * nvc >= (int64_t(1) << 31)) return hipErrorInvalidConfiguration;  // grid.x range
   auto kern = fwd_generic_ch_kernel<T>;
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), (int)smem);
   if (e != hipSuccess) return e;
@@ -628,6 +629,7 @@ hipError_t launch_bwd_generic_ch(const BwdArgs& a, hipStream_t stream) {
   if (e != hipSuccess) return e;
   const int64_t nkb = (nk + kGBK - 1) / kGBK;
   const int noc = (max(a.d, a.v_d) + kOC - 1) / kOC;
+  if (a.b * nkb * noc >= (int64_t(1) << 31)) return hipErrorInvalidConfiguration;  // grid.x range
   const size_t smem = sizeof(A) * ((size_t)kDC * (kGBQ + kGBK) + (size_t)kOC * (2 * kGBQ + kGBK) + 2 * kGBQ * (kGBK + 1) +
                                    2 * kGBQ);
   auto kern = bwd_generic_ch_kernel<T>;
@@ -681,7 +683,10 @@ hipError_t launch_bwd_generic(int dtype, const BwdArgs& a, hipStream_t s) {
 }
 
 // the channel-chunked kernels take any count; the cap only keeps a slice's channel rows (and the
-// dQ workspace index) well inside the int32 / int64 ranges the kernels use
+// dQ workspace index) well inside the int32 / int64 ranges the kernels use.  Their work grows as
+// d * max(d, v_d) / 256 (each chunk of output channels recomputes the full-d scores), so very wide
+// shapes are correct but slow; a grid past 2^31 blocks is refused (hipErrorInvalidConfiguration)
+// before the launch.
 int generic_max_channels(int dtype) { return (void)dtype, 65536; }
 
 }  // namespace fa
