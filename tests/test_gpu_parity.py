@@ -457,3 +457,26 @@ def test_f16_backward_read_placement(monkeypatch, diag_lib, variant, d, policy, 
     run_case(np.float16, policy, 1, "none_front", (2,), d, d, (328,), (264,), ws=ws, ls=0, causal=causal,
              seed=int(variant) + d)
     assert calls(1) == before + 1
+
+
+# the three-group rotation forward (fa_fwd_f16_trio.hip; full policy, d <= 64): 2501 hipcc-scheduled
+# MFMA phase, 2504 its fragment reads pinned between the MFMA pairs.  Shapes cross the 384-query
+# block (ragged last block, a block with idle waves), the key tail, d != v_d and d < 64.
+TRIO_CASES = [
+    ((2, 2), 64, 64, (384,), (256,)),
+    ((3,), 64, 64, (1000,), (1000,)),
+    ((2,), 48, 40, (130,), (72,)),
+    ((1,), 64, 48, (2000,), (64,)),
+    ((2,), 40, 64, (777,), (520,)),
+    ((2, 2), 32, 32, (400,), (384,)),
+    ((2,), 16, 8, (385,), (136,)),
+    ((3,), 8, 32, (100,), (1000,)),
+]
+
+
+@pytest.mark.parametrize("variant", ["2501", "2504", "2505", "2507", "2508"])
+@pytest.mark.parametrize("batch,d,vd,qs,ks", TRIO_CASES)
+def test_f16_trio_forward(monkeypatch, diag_lib, variant, batch, d, vd, qs, ks):
+    monkeypatch.setenv("FA_FWD_VARIANT", variant)
+    for mode in ("none_front", "scale_end"):
+        run_case(np.float16, "full", 1, mode, batch, d, vd, qs, ks, bwd=False, seed=int(variant) + d + vd)

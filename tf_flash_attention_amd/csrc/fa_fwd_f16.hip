@@ -487,6 +487,7 @@ hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s) {
     }
   }
   const bool pinned = v >= 0 && v < 1000;
+  if (v >= 2500 && v < 2600 && fwd_f16_trio_supported(a)) return launch_fwd_f16_trio(a, s);
 #else
   constexpr bool pinned = false;
 #endif

@@ -516,6 +516,7 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
   if (fwd_f16_pp_supported(a) && v >= 2000 && v < 2200) return launch_fwd_f16_pp(a, s);
   if (fwd_f16_pingpong_supported(a) && v >= 2200 && v < 2300) return launch_fwd_f16_pingpong(a, s);
   if (fwd_f16_pingpong128_supported(a) && v >= 2300 && v < 2400) return launch_fwd_f16_pingpong128(a, s);
+  if (fwd_f16_trio_supported(a) && v >= 2500 && v < 2600) return launch_fwd_f16_trio(a, s);
   if (d64 && v == 1899) {
     switch (diag_variant("FA_FWD_ABL")) {
       case 64: return launch_fast_t<64, 8, 6 | 64>(a, s);
