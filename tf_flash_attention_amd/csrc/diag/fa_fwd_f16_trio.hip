@@ -27,9 +27,13 @@
 // accumulation, log2-domain lazy rebase at 8, rebase check and m on the packed P, l relative to
 // the stored fp16 m).  Replaces the reference's ForwardImpl (flash_attention.cu:425-1077) for
 // these shapes.
-#include "fa_device.h"
-#include "fa_kernels.h"
-#include "fa_mfma.h"
+//
+// DIAGNOSTIC LIBRARY ONLY (measured and not taken): on config 2 it runs 0.58-0.61 ms
+// against 0.52-0.54 for the ping-pong kernel; without its fragment reads and staging (timing
+// ablations 2510-2512, outputs wrong) 0.449 ms, about what the ping-pong reaches without its LDS side.
+#include "../fa_device.h"
+#include "../fa_kernels.h"
+#include "../fa_mfma.h"
 
 namespace fa {
 namespace {
@@ -63,6 +67,9 @@ constexpr int kFPre = 8;
 // re-read per k-step inside each MFMA phase (one ds_read_b128 each): 16 fewer live registers
 // outside the MFMA phase
 constexpr int kFQLds = 16;
+// timing ablations (diagnostic library only; outputs WRONG): no K / V fragment reads in the MFMA
+// phase (the Q fragments stand in), no staging loads / stores
+constexpr int kANoFrag = 32, kANoStage = 64;
 
 template <int D, int F>
 __global__ __launch_bounds__(kNW * 64, 3) void fwd_f16_trio_kernel(FwdArgs a) {
@@ -328,10 +335,12 @@ __global__ __launch_bounds__(kNW * 64, 3) void fwd_f16_trio_kernel(FwdArgs a) {
     constexpr int c = decltype(C_)::value;  // it & 1
     if (F & kFPrio) __builtin_amdgcn_s_setprio(1);
     // K(i+1) over K(i-1) (read in the previous round), V(i) over V(i-2)
-    store(kdst[c ^ 1], kst);
-    store(vdst[c], vst);
-    kst = load(krs, koff, (it + 2) * kBN);
-    vst = load(vrs, voff, (it + 1) * kBN);
+    if constexpr ((F & kANoStage) == 0) {
+      store(kdst[c ^ 1], kst);
+      store(vdst[c], vst);
+      kst = load(krs, koff, (it + 2) * kBN);
+      vst = load(vrs, voff, (it + 1) * kBN);
+    }
     const lds_char_t* pk = smem + kOffK + c * kTile;
     const lds_char_t* pv = smem + kOffV + (c ^ 1) * kTile;
     half8 kf[kKS][2];
@@ -343,6 +352,10 @@ __global__ __launch_bounds__(kNW * 64, 3) void fwd_f16_trio_kernel(FwdArgs a) {
           kf[s][t] = kf0[t];
           continue;
         }
+        if (F & kANoFrag) {
+          kf[s][t] = qf[s];
+          continue;
+        }
         kf[s][t].lo = tr_read(pk + kbase[t] + (16 * s) * 128);
         kf[s][t].hi = tr_read(pk + kbase[t] + (16 * s + 4) * 128);
       }
@@ -350,7 +363,7 @@ __global__ __launch_bounds__(kNW * 64, 3) void fwd_f16_trio_kernel(FwdArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int u = 0; u < kU; ++u) vf[s][u] = read_b128(pv + vbase[s] + 32 * u * 128);
+      for (int u = 0; u < kU; ++u) vf[s][u] = (F & kANoFrag) ? qf[(s + u) % kKS] : read_b128(pv + vbase[s] + 32 * u * 128);
 #pragma unroll
     for (int s = 0; s < kKS; ++s) {
       const half8 qs = (F & kFQLds) ? read_b128(smem + qlo + 1024 * s) : qf[s];
@@ -499,7 +512,6 @@ bool fwd_f16_trio_supported(const FwdArgs& a) {
 constexpr int kFDefault = kFPrio;
 
 hipError_t launch_fwd_f16_trio(const FwdArgs& a, hipStream_t s) {
-#ifdef FA_DIAG
   switch (diag_variant("FA_FWD_VARIANT")) {
     case 2500: return launch_t<0>(a, s);
     case 2501: return launch_t<kFPrio>(a, s);
@@ -511,9 +523,13 @@ hipError_t launch_fwd_f16_trio(const FwdArgs& a, hipStream_t s) {
     case 2507: return launch_t<kFPrio | kFQLds>(a, s);
     case 2508: return launch_t<kFPrio | kFQLds | kFPre>(a, s);
     case 2509: return launch_t<kFPrio | kFQLds | kFPre | kFStamp>(a, s);
+    case 2510: return launch_t<kFPrio | kANoFrag>(a, s);
+    case 2511: return launch_t<kFPrio | kANoStage>(a, s);
+    case 2512: return launch_t<kFPrio | kANoFrag | kANoStage>(a, s);
+    case 2513: return launch_t<kFPrio | kANoFrag | kANoStage | kFStamp>(a, s);
+    case 2514: return launch_t<kFStamp>(a, s);
     default: break;
   }
-#endif
   return launch_t<kFDefault>(a, s);
 }
 

@@ -38,7 +38,23 @@ __device__ __forceinline__ void valu_units() {
 // (t + g) % R == 0, else its share of a softmax (8 units / (R-1)).
 // SPLIT (R = 2 only): the MFMA wave also issues half of a softmax (one half unit after each MFMA
 // pair) and the VALU wave the other half (4 units): the split-softmax ping-pong.
-template <int R, bool SPLIT = false>
+// ACC: 0 = compiler's choice (builtin), 1 = accumulators in arch VGPRs, 2 = in AGPRs, 3 = one of each
+// (the Sᵀ chain in VGPRs for the softmax, the PV chain in AGPRs), all by inline asm
+template <int ACC>
+__device__ __forceinline__ void mfma2(floatx16& c0, floatx16& c1, half8 a, half8 b) {
+  if constexpr (ACC == 0) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c1, 0, 0, 0);
+  } else if constexpr (ACC == 1) {
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %3, %0\n\tv_mfma_f32_32x32x16_f16 %1, %2, %3, %1" : "+v"(c0), "+v"(c1) : "v"(a), "v"(b));
+  } else if constexpr (ACC == 2) {
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %3, %0\n\tv_mfma_f32_32x32x16_f16 %1, %2, %3, %1" : "+a"(c0), "+a"(c1) : "v"(a), "v"(b));
+  } else {
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %3, %0\n\tv_mfma_f32_32x32x16_f16 %1, %2, %3, %1" : "+v"(c0), "+a"(c1) : "v"(a), "v"(b));
+  }
+}
+
+template <int R, bool SPLIT = false, int ACC = 0>
 __global__ __launch_bounds__(256 * R) void rot(unsigned long long* out, int iters) {
   half8 a, b;
   for (int i = 0; i < 8; ++i) { a[i] = (_Float16)(threadIdx.x * 1e-3f + i); b[i] = (_Float16)(i * 1e-2f); }
@@ -56,8 +72,7 @@ __global__ __launch_bounds__(256 * R) void rot(unsigned long long* out, int iter
       if ((ph + g) % R == 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c1, 0, 0, 0);
+          mfma2<ACC>(c0, c1, a, b);
           if constexpr (SPLIT) {
             __builtin_amdgcn_sched_barrier(0);
             asm volatile(HALF_UNIT ::: CLOBS);
@@ -95,7 +110,7 @@ __global__ __launch_bounds__(256 * W) void valu_only(unsigned long long* out, in
   if (threadIdx.x % 64 == 0) out[(blockIdx.x * 4 * W + threadIdx.x / 64) * 2] = t1 - t0;
 }
 
-template <int R, bool SPLIT = false>
+template <int R, bool SPLIT = false, int ACC = 0>
 void run_rot(unsigned long long* out, unsigned long long* host) {
   const int iters = 4000, blocks = 256;
   hipEvent_t e0, e1;
@@ -104,7 +119,7 @@ void run_rot(unsigned long long* out, unsigned long long* host) {
   float ms = 0;
   for (int rep = 0; rep < 3; ++rep) {
     (void)hipEventRecord(e0);
-    hipLaunchKernelGGL((rot<R, SPLIT>), dim3(blocks), dim3(256 * R), 0, 0, out, iters);
+    hipLaunchKernelGGL((rot<R, SPLIT, ACC>), dim3(blocks), dim3(256 * R), 0, 0, out, iters);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     (void)hipEventElapsedTime(&ms, e0, e1);
@@ -117,8 +132,8 @@ void run_rot(unsigned long long* out, unsigned long long* host) {
   const double ghz = cyc / rt / 10.0;  // s_memrealtime runs at 100 MHz
   // matrix work: one tile (16 MFMAs) per SIMD per interval
   const double flops = 2.0 * 32 * 32 * 16 * 16 * 4 * blocks * intervals;
-  printf("{\"roles\": %d, \"split\": %d, \"cycles_per_interval\": %.1f, \"clock_ghz\": %.3f, \"tflops\": %.1f}\n", R,
-         (int)SPLIT, per, ghz,
+  printf("{\"roles\": %d, \"split\": %d, \"acc\": %d, \"cycles_per_interval\": %.1f, \"clock_ghz\": %.3f, \"tflops\": %.1f}\n", R,
+         (int)SPLIT, ACC, per, ghz,
          flops / ms / 1e9);
 }
 
@@ -145,11 +160,12 @@ int main() {
   run_valu<2>(out, host);
   run_valu<3>(out, host);
   run_rot<2>(out, host);
-  run_rot<3>(out, host);
-  run_rot<4>(out, host);
-  run_rot<2, true>(out, host);
-  run_rot<2>(out, host);
-  run_rot<3>(out, host);
-  run_rot<2, true>(out, host);
+  run_rot<2, false, 1>(out, host);
+  run_rot<2, false, 2>(out, host);
+  run_rot<2, false, 3>(out, host);
+  run_rot<2, false, 0>(out, host);
+  run_rot<3, false, 2>(out, host);
+  run_rot<2, false, 1>(out, host);
+  run_rot<2, false, 2>(out, host);
   return 0;
 }
