@@ -86,7 +86,14 @@ constexpr int kMaxTStag = 22;
 // MFMA(0); O into LDS there too for group 1, at the head of MFMA(1) for group 0 (each beside the
 // other group's first softmax, instead of stretching its own VALU(0))
 constexpr int kBEpiSplit = 256;
-constexpr int kBandDefault = kBFPMax | kBStag | kBEpiSplit;  // round 3: staggered groups, split epilogue
+// the exponentials of a P k-step (8) issued as one batch into their own registers before its four
+// conversions: at ~235 VGPRs hipcc reused two temporaries, so every v_cvt_pk_f16_f32 waited on the
+// v_exp_f32 just before it (an s_nop plus the transcendental latency, 16 times a tile)
+constexpr int kBExpBatch = 1024;
+constexpr int kBandR3Final = kBFPMax | kBStag | kBEpiSplit;  // round 3: staggered groups, split epilogue
+// round 4: + exponentials in batches (c4, one process: 4.109-4.147 against 4.139-4.194 ms; outputs
+// bitwise unchanged)
+constexpr int kBandDefault = kBandR3Final | kBExpBatch;
 constexpr int kBandR3 = kBFPMax;                             // round 3 before the stagger: T positions for T tiles
 
 // staggered staging schedule (T positions, NT = T + 2 tiles an item, rings of four slots: tile j in
@@ -466,6 +473,19 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     }
   };
   auto exp_cvt = [&]() __attribute__((always_inline)) {
+    if constexpr ((F & kBExpBatch) != 0) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        float e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) e[j] = __builtin_amdgcn_exp2f(st[s >> 1][8 * (s & 1) + j]);
+        asm volatile("" : "+v"(e[0]), "+v"(e[1]), "+v"(e[2]), "+v"(e[3]), "+v"(e[4]), "+v"(e[5]), "+v"(e[6]), "+v"(e[7]));
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+          pw[s][x] = __builtin_bit_cast(uint32_t, half2v{(_Float16)e[2 * x], (_Float16)e[2 * x + 1]});
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -766,20 +786,27 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       const bool on = prv_q0 < nq;
       const lds_char_t* ob = smem + ((n + 1) & 1) * kQImg;
       const int tt = opaque_tid(), orw = tt >> 5, ocl = tt & 31;  // 16-B chunk (c = orw + 16j, queries 8*ocl..)
+      // the item's offsets are wave-uniform; readfirstlane proves it to hipcc (else every store below
+      // is wrapped in a waterfall loop with an lgkmcnt(0) inside: cdna_hip_programming.md T20)
+      const int osoff = __builtin_amdgcn_readfirstlane(prv_sl * osl + 2 * min(prv_q0, nq));
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int cc = orw + 16 * (2 * (it & 1) + j);
         const u32x4 v = *reinterpret_cast<const lds_u32x4_t*>(ob + cc * kQRow + 16 * ocl);
         const bool in = on && prv_q0 + 8 * ocl < nq;
         __builtin_amdgcn_raw_buffer_store_b128(v, ors, in ? (uint32_t)cc * (uint32_t)nq * 2u + 16u * ocl : 0x80000000u,
-                                               prv_sl * osl + 2 * min(prv_q0, nq), 0);
+                                               osoff, 0);
       }
       if constexpr (it == 2) {
-        const u32x4 v = *reinterpret_cast<const lds_u32x4_t*>(smem + kOffLM + 16 * (tt % 96));
+        // l (64 chunks of 4 queries) from threads 0-63, m (32 chunks of 8) from threads 64-95
+        const int lmc = tt < 64 ? tt : (tt < 96 ? tt : 0);
+        const u32x4 v = *reinterpret_cast<const lds_u32x4_t*>(smem + kOffLM + 16 * lmc);
         const uint32_t loff = (on && tt < 64 && prv_q0 + 4 * tt < nq) ? 16u * tt : 0x80000000u;
         const uint32_t moff = (on && tt >= 64 && tt < 96 && prv_q0 + 8 * (tt - 64) < nq) ? 16u * (tt - 64) : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b128(v, lrs, loff, prv_sl * 4 * nq + 4 * min(prv_q0, nq), 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v, mrs, moff, prv_sl * 2 * nq + 2 * min(prv_q0, nq), 0);
+        const int lsoff = __builtin_amdgcn_readfirstlane(prv_sl * 4 * nq + 4 * min(prv_q0, nq));
+        const int msoff = __builtin_amdgcn_readfirstlane(prv_sl * 2 * nq + 2 * min(prv_q0, nq));
+        __builtin_amdgcn_raw_buffer_store_b128(v, lrs, loff, lsoff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, mrs, moff, msoff, 0);
       }
     }
     if constexpr (it >= 2 && it <= 5) qst = qload(nxt, it - 2);
@@ -1041,7 +1068,8 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
     }
   }
   if (dv == 2421 && ba.T == 10) return launch_band_t<10, true>(ba, s);
-  if (dv == 2422 && ba.T == 10) return launch_band_t<10, false, kBFPMax | kBStag>(ba, s);  // epilogue in VALU(0)
+  if (dv == 2422 && ba.T == 10) return launch_band_t<10, false, kBFPMax | kBStag | kBExpBatch>(ba, s);  // epilogue in VALU(0)
+  if (dv == 2424 && ba.T == 10) return launch_band_t<10, false, kBandR3Final>(ba, s);  // round-3 default
 #endif
   switch (ba.T) {
     case 10: return launch_band_t<10>(ba, s);
