@@ -131,6 +131,14 @@ __host__ __device__ constexpr int stag_v1(int T, int p, int g, int i) {
 __host__ __device__ constexpr int stag_nk(int T, int p) { return (p == 0 || p >= T - 2) ? 2 : 1; }
 __host__ __device__ constexpr int stag_nv(int T, int p) { return (p <= 1 || p == T - 1) ? 2 : 1; }
 constexpr float kRescaleThr = 8.f;
+// after a 16-B buffer store: a wait state before any VALU may overwrite its data VGPRs (hipcc,
+// ROCm 7.2, emitted such a write as the very next instruction and the stored dword arrived corrupted:
+// DESIGN.md §6 toolchain finding (b); tools/check_store_hazard.py checks the shipped library)
+__device__ __forceinline__ void store_data_guard() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 // masked scores sit at or below -2^99 (the arithmetic edge mask); a row maximum at or below this
 // floor means "nothing allowed yet" (never a reference), and is the unset state of thr.  Every
 // finite score formed from fp16 inputs lies far inside (-2^98, 2^99), so no allowed score is clipped
@@ -796,6 +804,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         const bool in = on && prv_q0 + 8 * ocl < nq;
         __builtin_amdgcn_raw_buffer_store_b128(v, ors, in ? (uint32_t)cc * (uint32_t)nq * 2u + 16u * ocl : 0x80000000u,
                                                osoff, 0);
+        store_data_guard();
       }
       if constexpr (it == 2) {
         // l (64 chunks of 4 queries) from threads 0-63, m (32 chunks of 8) from threads 64-95
@@ -806,7 +815,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         const int lsoff = __builtin_amdgcn_readfirstlane(prv_sl * 4 * nq + 4 * min(prv_q0, nq));
         const int msoff = __builtin_amdgcn_readfirstlane(prv_sl * 2 * nq + 2 * min(prv_q0, nq));
         __builtin_amdgcn_raw_buffer_store_b128(v, lrs, loff, lsoff, 0);
+        store_data_guard();
         __builtin_amdgcn_raw_buffer_store_b128(v, mrs, moff, msoff, 0);
+        store_data_guard();
       }
     }
     if constexpr (it >= 2 && it <= 5) qst = qload(nxt, it - 2);
