@@ -306,6 +306,20 @@ def test_wide_channels(dtype, d, vd, policy, ws, causal):
     run_case(dtype, policy, 1, "scale_front", (2,), d, vd, (97,), (150,), ws=ws, causal=causal, seed=d + vd)
 
 
+# fp16 forward for 128 < max(d, v_d) <= 256 on MFMA (fa_fwd_f16_wide.hip: full and interval rules,
+# nk % 8 == 0, aligned K / V): several key tiles, ragged query blocks, d != v_d, every sync mode
+@pytest.mark.parametrize("d,vd", [(256, 256), (160, 160), (130, 200), (200, 64), (64, 256)])
+@pytest.mark.parametrize("policy,mode,qs,ks,ws,causal", [
+    ("full", "none_front", (300,), (520,), 1, False),
+    ("causal", "none_front", (777,), (777,), 1, False),
+    ("causal", "scale_end", (200,), (520,), 1, False),
+    ("local", "scale_front", (240,), (480,), 70, True),
+    ("local", "none_front", (700,), (704,), 33, False),
+])
+def test_wide_channels_mfma_forward(d, vd, policy, mode, qs, ks, ws, causal):
+    run_case(np.float16, policy, 1, mode, (2,), d, vd, qs, ks, ws=ws, causal=causal, bwd=False, seed=d + 3 * vd)
+
+
 # --------------------------------------------------------------- edge cases
 @pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
 @pytest.mark.parametrize("nq,nk", [(1, 1), (1, 77), (77, 1), (2, 3), (64, 64), (65, 63)])

@@ -466,11 +466,14 @@ hipError_t launch_t(const FwdArgs& a, hipStream_t s) {
 }  // namespace
 
 bool fwd_f16_supported(const FwdArgs& a) {
+  if (fwd_f16_wide_supported(a)) return true;
   return a.d >= 1 && a.v_d >= 1 && a.d <= 128 && a.v_d <= 128 && a.b * ((a.rule.q.n + 127) / 128) < (1ll << 31);
 }
 
 hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s) {
   const int dm = max(a.d, a.v_d);
+  // 128 < max(d, v_d) <= 256 under the full / interval rules with aligned K, V: 256-channel MFMA tiles
+  if (dm > 128) return launch_fwd_f16_wide(a, s);
 #ifdef FA_DIAG
   // FA_FWD_VARIANT = <NW><F> below 1000 pins this general kernel (A/B runs), e.g. 408
   const int v = diag_variant("FA_FWD_VARIANT");

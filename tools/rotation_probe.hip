@@ -54,7 +54,8 @@ __device__ __forceinline__ void mfma2(floatx16& c0, floatx16& c1, half8 a, half8
   }
 }
 
-template <int R, bool SPLIT = false, int ACC = 0>
+// PRIO: 0 none, 1 the MFMA phase at s_setprio 1, 2 the VALU phases at s_setprio 1
+template <int R, bool SPLIT = false, int ACC = 0, int PRIO = 0>
 __global__ __launch_bounds__(256 * R) void rot(unsigned long long* out, int iters) {
   half8 a, b;
   for (int i = 0; i < 8; ++i) { a[i] = (_Float16)(threadIdx.x * 1e-3f + i); b[i] = (_Float16)(i * 1e-2f); }
@@ -70,6 +71,7 @@ __global__ __launch_bounds__(256 * R) void rot(unsigned long long* out, int iter
 #pragma unroll
     for (int ph = 0; ph < R; ++ph) {
       if ((ph + g) % R == 0) {
+        if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           mfma2<ACC>(c0, c1, a, b);
@@ -79,11 +81,14 @@ __global__ __launch_bounds__(256 * R) void rot(unsigned long long* out, int iter
             __builtin_amdgcn_sched_barrier(0);
           }
         }
+        if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
       } else {
+        if (PRIO == 2) __builtin_amdgcn_s_setprio(1);
         if constexpr (R == 2 && SPLIT) valu_units<4>();
         if constexpr (R == 2 && !SPLIT) valu_units<8>();
         if constexpr (R == 3) valu_units<4>();
         if constexpr (R == 4) { valu_units<3>(); }
+        if (PRIO == 2) __builtin_amdgcn_s_setprio(0);
       }
       __syncthreads();
     }
@@ -110,7 +115,7 @@ __global__ __launch_bounds__(256 * W) void valu_only(unsigned long long* out, in
   if (threadIdx.x % 64 == 0) out[(blockIdx.x * 4 * W + threadIdx.x / 64) * 2] = t1 - t0;
 }
 
-template <int R, bool SPLIT = false, int ACC = 0>
+template <int R, bool SPLIT = false, int ACC = 0, int PRIO = 0>
 void run_rot(unsigned long long* out, unsigned long long* host) {
   const int iters = 4000, blocks = 256;
   hipEvent_t e0, e1;
@@ -119,7 +124,7 @@ void run_rot(unsigned long long* out, unsigned long long* host) {
   float ms = 0;
   for (int rep = 0; rep < 3; ++rep) {
     (void)hipEventRecord(e0);
-    hipLaunchKernelGGL((rot<R, SPLIT, ACC>), dim3(blocks), dim3(256 * R), 0, 0, out, iters);
+    hipLaunchKernelGGL((rot<R, SPLIT, ACC, PRIO>), dim3(blocks), dim3(256 * R), 0, 0, out, iters);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     (void)hipEventElapsedTime(&ms, e0, e1);
@@ -132,8 +137,8 @@ void run_rot(unsigned long long* out, unsigned long long* host) {
   const double ghz = cyc / rt / 10.0;  // s_memrealtime runs at 100 MHz
   // matrix work: one tile (16 MFMAs) per SIMD per interval
   const double flops = 2.0 * 32 * 32 * 16 * 16 * 4 * blocks * intervals;
-  printf("{\"roles\": %d, \"split\": %d, \"acc\": %d, \"cycles_per_interval\": %.1f, \"clock_ghz\": %.3f, \"tflops\": %.1f}\n", R,
-         (int)SPLIT, ACC, per, ghz,
+  printf("{\"roles\": %d, \"split\": %d, \"acc\": %d, \"prio\": %d, \"cycles_per_interval\": %.1f, \"clock_ghz\": %.3f, \"tflops\": %.1f}\n", R,
+         (int)SPLIT, ACC, PRIO, per, ghz,
          flops / ms / 1e9);
 }
 
@@ -156,16 +161,11 @@ int main() {
   (void)hipMalloc(&out, 256 * 16 * 16);
   host = (unsigned long long*)malloc(256 * 16 * 16);
   run_valu<1>(out, host);
-  run_valu<1>(out, host);
-  run_valu<2>(out, host);
-  run_valu<3>(out, host);
-  run_rot<2>(out, host);
-  run_rot<2, false, 1>(out, host);
-  run_rot<2, false, 2>(out, host);
-  run_rot<2, false, 3>(out, host);
-  run_rot<2, false, 0>(out, host);
-  run_rot<3, false, 2>(out, host);
-  run_rot<2, false, 1>(out, host);
-  run_rot<2, false, 2>(out, host);
+  run_rot<2, false, 0, 0>(out, host);
+  run_rot<2, false, 0, 1>(out, host);
+  run_rot<2, false, 0, 2>(out, host);
+  run_rot<2, false, 0, 0>(out, host);
+  run_rot<2, false, 0, 1>(out, host);
+  run_rot<2, false, 0, 2>(out, host);
   return 0;
 }

@@ -1,0 +1,49 @@
+"""Forward time at 256 channels (config 2's shape at d = 256): the MFMA kernel (fa_fwd_f16_wide.hip)
+against the SIMT kernel the same call took before round 4 (reached here through a K / V pointer one
+element off 16-B alignment, which the MFMA kernel does not take).  Usage: python tools/wide_time.py"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tf_flash_attention_amd import flash_attention as fa  # noqa: E402
+
+
+def timed(fn, n=10):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    return sorted(a.elapsed_time(b) for a, b in ev)[n // 2]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    b, d, n = 128, 256, 4096
+    g = torch.Generator(device=dev).manual_seed(0)
+    q = (torch.rand((b, d, n), generator=g, device=dev) * 4 - 2).half()
+    k = (torch.rand((b, d, n), generator=g, device=dev) * 4 - 2).half()
+    v = (torch.rand((b, d, n), generator=g, device=dev) * 4 - 2).half()
+    kb = torch.empty(k.numel() + 1, dtype=k.dtype, device=dev)
+    kb[1:].copy_(k.reshape(-1))
+    km = kb[1:].view(k.shape)
+    flops = 2.0 * (d + d) * n * n * b
+    t_mfma = timed(lambda: fa.attention_forward("full", 1, q, k, v, "none_front", 1, 0, False))
+    o1, _, _ = fa.attention_forward("full", 1, q, k, v, "none_front", 1, 0, False)
+    t_simt = timed(lambda: fa.attention_forward("full", 1, q, km, v, "none_front", 1, 0, False), n=3)
+    o2, _, _ = fa.attention_forward("full", 1, q, km, v, "none_front", 1, 0, False)
+    print(json.dumps({"shape": "full_1d fp16 b=128 d=256 n=4096", "mfma_ms": round(t_mfma, 4),
+                      "mfma_tflops": round(flops / t_mfma / 1e9, 1), "simt_ms": round(t_simt, 4),
+                      "simt_tflops": round(flops / t_simt / 1e9, 1),
+                      "max_abs_diff": float((o1.float() - o2.float()).abs().max())}))
+
+
+if __name__ == "__main__":
+    main()
