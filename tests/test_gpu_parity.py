@@ -320,6 +320,21 @@ def test_wide_channels_mfma_forward(d, vd, policy, mode, qs, ks, ws, causal):
     run_case(np.float16, policy, 1, mode, (2,), d, vd, qs, ks, ws=ws, causal=causal, bwd=False, seed=d + 3 * vd)
 
 
+# fp16 backward for 128 < max(d, v_d) <= 256 on MFMA (fa_bwd_f16_fast.hip launch_bwd_wide: the one-wave
+# dK / dV and dQ passes at D = 256, two 128-channel output chunks per slice; aligned tensors, lengths
+# multiples of 8, every rule incl. 2-D windows)
+@pytest.mark.parametrize("d,vd", [(256, 256), (160, 160), (136, 256), (256, 64), (72, 200)])
+@pytest.mark.parametrize("policy,seq,mode,qs,ks,ws,ls,causal", [
+    ("full", 1, "none_front", (264,), (520,), 1, 1, False),
+    ("causal", 1, "none_front", (392,), (392,), 1, 1, False),
+    ("causal", 1, "scale_end", (200,), (520,), 1, 1, False),
+    ("local", 1, "scale_front", (240,), (480,), 70, 1, True),
+    ("local", 2, "none_front", (16, 24), (16, 24), 5, 3, True),
+])
+def test_wide_channels_mfma_backward(d, vd, policy, seq, mode, qs, ks, ws, ls, causal):
+    run_case(np.float16, policy, seq, mode, (2,), d, vd, qs, ks, ws=ws, ls=ls, causal=causal, seed=d + 5 * vd)
+
+
 # --------------------------------------------------------------- edge cases
 @pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
 @pytest.mark.parametrize("nq,nk", [(1, 1), (1, 77), (77, 1), (2, 3), (64, 64), (65, 63)])

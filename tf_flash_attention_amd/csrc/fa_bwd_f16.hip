@@ -352,6 +352,7 @@ hipError_t launch_main(const BwdArgs& a, hipStream_t s) {
 }  // namespace
 
 bool bwd_f16_supported(const BwdArgs& a) {
+  if (max(a.d, a.v_d) > 128) return bwd_f16_fast_supported(a);  // the 256-channel two-pass kernels
   return a.d >= 1 && a.v_d >= 1 && a.d <= 128 && a.v_d <= 128 &&
          a.b * ((a.rule.k.n + kBK - 1) / kBK) < (1ll << 31);
 }

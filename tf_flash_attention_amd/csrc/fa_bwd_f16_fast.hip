@@ -97,7 +97,10 @@ struct DkdvSmem {
 // ---------------------------------------------------------------------------
 // dK / dV: key-outer.  One workgroup = NW waves x 32 keys of one (batch, head) slice (the d <= 64
 // pass, two waves per SIMD; d = 128 runs the producer / consumer pass below).
-template <int D, int NW, int WPE, int POL, bool ALN>
+// OC > 1 (128 < d <= 256): the workgroup accumulates dK / dV for one of OC chunks of D / OC output
+// channels (chunk = block index mod OC), forming S and dP over all D channels as before: the 256-channel
+// accumulators of both gradients would not fit one wave beside the resident K' and V.
+template <int D, int NW, int WPE, int POL, bool ALN, int OC = 1>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -108,9 +111,12 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   static_assert((2 * kQChunks) % kThr == 0, "tile chunks must divide over the workgroup");
   constexpr int kCPT = 2 * kQChunks / kThr;           // Q and dO chunks per thread
 
+  constexpr int kDO = D / OC;                         // output channels of this workgroup
   const int nq = a.rule.q.n, nk = a.rule.k.n;
   const uint32_t nkb = (nk + kBK - 1) / kBK;
-  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t bidc = xcd_remap(blockIdx.x, gridDim.x);
+  const int oc = (int)(bidc % OC), ou0 = oc * (kDO / 32);  // the chunk: channel blocks ou0 .. ou0 + kDO/32 - 1
+  const uint32_t bid = bidc / OC;
   const int64_t bi = bid / nkb;
   const int k0 = (int)(bid % nkb) * kBK;  // earliest (heaviest under causal) key blocks first
   const int tid = threadIdx.x, lane = tid & 63;
@@ -250,9 +256,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
     if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr[set];
   };
 
-  floatx16 dk[D / 32], dv[D / 32];
+  floatx16 dk[kDO / 32], dv[kDO / 32];
 #pragma unroll
-  for (int u = 0; u < D / 32; ++u)
+  for (int u = 0; u < kDO / 32; ++u)
 #pragma unroll
     for (int i = 0; i < 16; ++i) { dk[u][i] = 0.f; dv[u][i] = 0.f; }
 
@@ -320,9 +326,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int u = 0; u < D / 32; ++u) {
-        const half8 oa = read_b128(base + S::offOT + q16_off(32 * u + r, 2 * s + h));
-        const half8 qa = read_b128(base + S::offQT + q16_off(32 * u + r, 2 * s + h));
+      for (int u = 0; u < kDO / 32; ++u) {
+        const half8 oa = read_b128(base + S::offOT + q16_off(32 * (ou0 + u) + r, 2 * s + h));
+        const half8 qa = read_b128(base + S::offQT + q16_off(32 * (ou0 + u) + r, 2 * s + h));
         dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa, pf[s], dv[u], 0, 0, 0);
         dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa, sf[s], dk[u], 0, 0, 0);
       }
@@ -371,20 +377,20 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
     const __amdgpu_buffer_rsrc_t krs_ = make_rsrc(dK, 2u * d * nk), vrs_ = make_rsrc(dV, 2u * vd * nk);
     const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nk + (uint32_t)key);
 #pragma unroll
-    for (int u = 0; u < D / 32; ++u)
+    for (int u = 0; u < kDO / 32; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const uint32_t so = 2u * (32u * u + (i & 3) + 8u * (i >> 2)) * (uint32_t)nk;
+        const uint32_t so = 2u * (32u * (ou0 + u) + (i & 3) + 8u * (i >> 2)) * (uint32_t)nk;
         __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(dk[u][i] * sc)), krs_, vlane, so, 0);
         __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)dv[u][i]), vrs_, vlane, so, 0);
       }
     return;
   }
 #pragma unroll
-  for (int u = 0; u < D / 32; ++u)
+  for (int u = 0; u < kDO / 32; ++u)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+      const int c = 32 * (ou0 + u) + (i & 3) + 8 * (i >> 2) + 4 * h;
       if (c < d) dK[(int64_t)c * nk + key] = __float2half(dk[u][i] * sc);
       if (c < vd) dV[(int64_t)c * nk + key] = __float2half(dv[u][i]);
     }
@@ -792,7 +798,11 @@ struct DqSmem {
 };
 
 // dQ: query-outer.  One workgroup = NW waves x 32 queries of one (batch, head) slice.
-template <int D, int NW, int WPE, int POL, bool ALN, bool PRE = false, bool MSPEC = false>
+// OC > 1 (128 < d <= 256): the workgroup accumulates dQ for one of OC chunks of D / OC channels (chunk =
+// block index mod OC), recomputing Sᵀ and dPᵀ over all D channels.  ONESET: one staging register set
+// (tile it+1 loaded at the head of step it and stored after its MFMAs, into the slot tile it-1 left)
+// instead of two sets loaded two steps ahead: at D = 256 a set is 64 registers.
+template <int D, int NW, int WPE, int POL, bool ALN, bool PRE = false, bool MSPEC = false, int OC = 1, bool ONESET = false>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -805,9 +815,12 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   constexpr int kCPT = 2 * kKChunks / kThr;           // K and V chunks per thread
   constexpr float kNegInf = -__builtin_huge_valf();
 
+  constexpr int kDO = D / OC;  // dQ channels of this workgroup
   const int nq = a.rule.q.n, nk = a.rule.k.n;
   const uint32_t nqb = (nq + kBM - 1) / kBM;
-  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t bidc = xcd_remap(blockIdx.x, gridDim.x);
+  const int oc = (int)(bidc % OC), ou0 = oc * (kDO / 32);
+  const uint32_t bid = bidc / OC;
   const int64_t bi = bid / nqb;
   const int q0 = (int)(nqb - 1 - (bid % nqb)) * kBM;  // latest (heaviest under causal) blocks first
   const int tid = threadIdx.x, lane = tid & 63;
@@ -918,7 +931,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     voff[j] = (uint32_t)crow_[j] * (uint32_t)nk * 2u + (ALN ? 16u * cm : 0u);  // (ALN: the chunk's; else the row's)
   }
   // two staging sets (tile t in set t&1): a tile is loaded two steps before it is stored
-  u32x4 kr[2][kCPT];
+  u32x4 kr[ONESET ? 1 : 2][kCPT];
   auto is_v = [&](int j) -> bool {
     return (kKChunks % kThr == 0) ? (j >= kKChunks / kThr) : ((tid + kThr * j) >= kKChunks);
   };
@@ -941,9 +954,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
       *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + k2_off(crow_[j], cm)) = kr[set][j];
     }
   };
-  floatx16 dq[D / 32];
+  floatx16 dq[kDO / 32];
 #pragma unroll
-  for (int u = 0; u < D / 32; ++u)
+  for (int u = 0; u < kDO / 32; ++u)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[u][i] = 0.f;
 
@@ -964,8 +977,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
   // state merged, and the loop's first step then drained every load in flight
   load_tile(kt0, 0);
   store_tile(0, 0);
-  load_tile(kt0 + kBN, 1);
-  load_tile(kt0 + 2 * kBN, 0);
+  if constexpr (!ONESET) {
+    load_tile(kt0 + kBN, 1);
+    load_tile(kt0 + 2 * kBN, 0);
+  }
 
   auto step = [&](auto P_, int it) {
     constexpr int p = decltype(P_)::value;
@@ -973,16 +988,24 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     const int ka = kt0 + it * kBN;
     const int cls = it < ntiles ? tcls(ka) : 0;  // (the loop's last pair may end on a phantom step)
     // unconditional (past the end they move zeros into a slot nobody reads): exact vmcnt waits
-    store_tile(p ^ 1, p ^ 1);
-    load_tile(ka + 3 * kBN, p ^ 1);
+    if constexpr (ONESET) {
+      load_tile(ka + kBN, 0);
+    } else {
+      store_tile(p ^ 1, p ^ 1);
+      load_tile(ka + 3 * kBN, p ^ 1);
+    }
+    struct StoreAtExit {  // ONESET: tile it+1 into slot p^1 after this step's MFMAs (on every return)
+      decltype(store_tile)& f;
+      __device__ ~StoreAtExit() { if constexpr (ONESET) f(p ^ 1, 0); }
+    } store_at_exit{store_tile};
     if (cls == 0) return;
     const lds_char_t* base = smem + p * S::kSlot;
     floatx16 st[2], dp[2];
     // PRE: every operand read two MFMA pairs ahead of its MFMAs (one wave per SIMD: nothing else
     // hides an LDS round trip between a read and the MFMA that consumes it)
     half8 ka8p[3];
-    auto rka = [&](int n) __attribute__((always_inline)) {  // dQ operand n = 4s + u
-      ka8p[n % 3] = read_b128(base + S::offKT + kb2[n / (D / 32)] + 32 * (n % (D / 32)) * 128);
+    auto rka = [&](int n) __attribute__((always_inline)) {  // dQ operand n = (kDO/32)·s + u
+      ka8p[n % 3] = read_b128(base + S::offKT + kb2[n / (kDO / 32)] + 32 * (ou0 + n % (kDO / 32)) * 128);
     };
     if constexpr (PRE) {
       constexpr int kN = 2 * (D / 16);
@@ -1039,13 +1062,13 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
         dsf[j] = (_Float16)(pv * dp[t][i]);
       }
 #pragma unroll
-      for (int u = 0; u < D / 32; ++u) {
+      for (int u = 0; u < kDO / 32; ++u) {
         if constexpr (PRE) {
-          const int n = (D / 32) * s + u;
-          if (n + 2 < 4 * (D / 32)) rka(n + 2);
+          const int n = (kDO / 32) * s + u;
+          if (n + 2 < 4 * (kDO / 32)) rka(n + 2);
           dq[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka8p[n % 3], dsf, dq[u], 0, 0, 0);
         } else {
-          const half8 ka8 = read_b128(base + S::offKT + kb2[s] + 32 * u * 128);
+          const half8 ka8 = read_b128(base + S::offKT + kb2[s] + 32 * (ou0 + u) * 128);
           dq[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka8, dsf, dq[u], 0, 0, 0);
         }
       }
@@ -1074,18 +1097,18 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dq_kernel(BwdArgs a) {
     const __amdgpu_buffer_rsrc_t qrs_ = make_rsrc(dQ, 2u * d * nq);
     const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nq + (uint32_t)qi);
 #pragma unroll
-    for (int u = 0; u < D / 32; ++u)
+    for (int u = 0; u < kDO / 32; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(dq[u][i] * sc)), qrs_, vlane,
-                                              2u * (32u * u + (i & 3) + 8u * (i >> 2)) * (uint32_t)nq, 0);
+                                              2u * (32u * (ou0 + u) + (i & 3) + 8u * (i >> 2)) * (uint32_t)nq, 0);
     return;
   }
 #pragma unroll
-  for (int u = 0; u < D / 32; ++u)
+  for (int u = 0; u < kDO / 32; ++u)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+      const int c = 32 * (ou0 + u) + (i & 3) + 8 * (i >> 2) + 4 * h;
       if (c < d) dQ[(int64_t)c * nq + qi] = __float2half(dq[u][i] * sc);
     }
 }
@@ -1538,6 +1561,34 @@ hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// 128 < max(d, v_d) <= 256 (16-B aligned tensors, lengths multiples of 8): both one-wave passes at D =
+// 256, each workgroup on one of two 128-channel output chunks
+hipError_t launch_bwd_wide(const BwdArgs& a, hipStream_t s) {
+  constexpr int D = 256, NW = 4, OC = 2;
+  const int pol = bwd_pol(a.rule);
+  {
+    using S = DkdvSmem<D, NW>;
+    const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
+    const BwdKernel kern = pol == 0   ? bwd_dkdv_kernel<D, NW, 1, 0, true, OC>
+                           : pol == 1 ? bwd_dkdv_kernel<D, NW, 1, 1, true, OC>
+                                      : bwd_dkdv_kernel<D, NW, 1, 2, true, OC>;
+    hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb * OC)), dim3(NW * 64), S::kTotal, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  using S = DqSmem<D, NW>;
+  const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
+  const BwdKernel kern = pol == 0   ? bwd_dq_kernel<D, NW, 1, 0, true, false, false, OC, true>
+                         : pol == 1 ? bwd_dq_kernel<D, NW, 1, 1, true, false, false, OC, true>
+                                    : bwd_dq_kernel<D, NW, 1, 2, true, false, false, OC, true>;
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb * OC)), dim3(NW * 64), S::kTotal, s, a);
+  return hipGetLastError();
+}
+
 template <int D, int PF = 0>
 hipError_t launch_dq_pc(const BwdArgs& a, hipStream_t s) {
   using S = DqPcSmem<D>;
@@ -1562,9 +1613,10 @@ bool bwd_f16_fast_supported(const BwdArgs& a) {
   const int dm = max(a.d, a.v_d);
   // (buffer offsets are 32-bit: a channel row set of one slice stays below 2^31 bytes; the element-wise
   // staging of the unaligned form addresses up to 2·n + 14 bytes past a row start)
-  return dm >= 1 && dm <= 128 && nq > 0 && nk > 0 && (int64_t)dm * (nq + 8) * 2 < (1ll << 31) &&
-         (int64_t)dm * (nk + 8) * 2 < (1ll << 31) && a.b * ((nk + 127) / 128) < (1ll << 31) &&
-         a.b * ((nq + 127) / 128) < (1ll << 31);
+  return dm >= 1 && (dm <= 128 || (dm <= 256 && bwd_aligned(a))) && nq > 0 && nk > 0 &&
+         (int64_t)dm * (nq + 8) * 2 < (1ll << 31) &&
+         (int64_t)dm * (nk + 8) * 2 < (1ll << 31) && a.b * ((nk + 127) / 128) * 2 < (1ll << 31) &&
+         a.b * ((nq + 127) / 128) * 2 < (1ll << 31);
 }
 
 hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
@@ -1572,6 +1624,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(bwd_prep_kernel, dim3((unsigned)((nrows + kThrPrep - 1) / kThrPrep)), dim3(kThrPrep), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (max(a.d, a.v_d) > 128) return launch_bwd_wide(a, s);
 #ifdef FA_DIAG
   // FA_BWD_VARIANT (diagnostic library): d <= 64 — 82 eight-wave blocks, 1068 / 1069 the dQ pass's
   // operand reads run ahead, 1071 its edge mask as a branch; d = 128 — 1404 the dK/dV pass's stamp

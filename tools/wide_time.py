@@ -1,6 +1,7 @@
-"""Forward time at 256 channels (config 2's shape at d = 256): the MFMA kernel (fa_fwd_f16_wide.hip)
-against the SIMT kernel the same call took before round 4 (reached here through a K / V pointer one
-element off 16-B alignment, which the MFMA kernel does not take).  Usage: python tools/wide_time.py"""
+"""Forward and backward time at 256 channels (config 2's shape at d = 256): the MFMA kernels
+(fa_fwd_f16_wide.hip; fa_bwd_f16_fast.hip launch_bwd_wide) against the SIMT kernels the same calls took
+before round 4 (reached here through a K pointer one element off 16-B alignment, which the MFMA kernels
+do not take).  Usage: python tools/wide_time.py [b] [n]"""
 import json
 import os
 import sys
@@ -26,7 +27,9 @@ def timed(fn, n=10):
 
 def main():
     dev = torch.device("cuda:0")
-    b, d, n = 128, 256, 4096
+    b = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    d = 256
     g = torch.Generator(device=dev).manual_seed(0)
     q = (torch.rand((b, d, n), generator=g, device=dev) * 4 - 2).half()
     k = (torch.rand((b, d, n), generator=g, device=dev) * 4 - 2).half()
@@ -39,10 +42,22 @@ def main():
     o1, _, _ = fa.attention_forward("full", 1, q, k, v, "none_front", 1, 0, False)
     t_simt = timed(lambda: fa.attention_forward("full", 1, q, km, v, "none_front", 1, 0, False), n=3)
     o2, _, _ = fa.attention_forward("full", 1, q, km, v, "none_front", 1, 0, False)
-    print(json.dumps({"shape": "full_1d fp16 b=128 d=256 n=4096", "mfma_ms": round(t_mfma, 4),
+    print(json.dumps({"shape": f"full_1d fp16 b={b} d={d} n={n}", "pass": "forward", "mfma_ms": round(t_mfma, 4),
                       "mfma_tflops": round(flops / t_mfma / 1e9, 1), "simt_ms": round(t_simt, 4),
                       "simt_tflops": round(flops / t_simt / 1e9, 1),
-                      "max_abs_diff": float((o1.float() - o2.float()).abs().max())}))
+                      "max_abs_diff": float((o1.float() - o2.float()).abs().max())}), flush=True)
+    # backward: dK / dV pass (4 matmuls) + dQ pass (3 matmuls: Sᵀ, dPᵀ recomputed, dQ) = 2.5x the forward
+    o1, l1, m1 = fa.attention_forward("full", 1, q, k, v, "none_front", 1, 0, False)
+    do = (torch.rand((b, d, n), generator=g, device=dev) * 4 - 2).half()
+    bflops = 2.5 * flops
+    t_bm = timed(lambda: fa.attention_backward("full", 1, q, k, v, o1, l1, m1, do, "none_front"))
+    g1 = fa.attention_backward("full", 1, q, k, v, o1, l1, m1, do, "none_front")
+    t_bs = timed(lambda: fa.attention_backward("full", 1, q, km, v, o1, l1, m1, do, "none_front"), n=3)
+    g2 = fa.attention_backward("full", 1, q, km, v, o1, l1, m1, do, "none_front")
+    diff = max(float((x.float() - y.float()).abs().max() / y.float().abs().max()) for x, y in zip(g1, g2))
+    print(json.dumps({"shape": f"full_1d fp16 b={b} d={d} n={n}", "pass": "backward", "mfma_ms": round(t_bm, 4),
+                      "mfma_tflops": round(bflops / t_bm / 1e9, 1), "simt_ms": round(t_bs, 4),
+                      "simt_tflops": round(bflops / t_bs / 1e9, 1), "max_rel_diff": diff}), flush=True)
 
 
 if __name__ == "__main__":
