@@ -55,6 +55,7 @@ CONFIGS = {
     "d32": ("full", 1, torch.float16, (8, 16), 32, (4096,), (4096,), "none_front", 1, 0, False, False, "weak"),
     # not a BASELINE config: config 2's shape at d = 256, past the d <= 128 kernels (fa_fwd_f16_wide.hip)
     "w256": ("full", 1, torch.float16, (8, 16), 256, (4096,), (4096,), "none_front", 1, 0, False, False, "weak"),
+    "w256b": ("causal", 1, torch.float16, (8, 16), 256, (8192,), (8192,), "none_front", 1, 0, False, True, "weak"),
 }
 WORKLOAD = {
     "c2": "full_1d fp16 B=8 H=16 d=64 Nq=Nk=4096 forward (BASELINE config 2)",
@@ -63,6 +64,7 @@ WORKLOAD = {
     "c5": "full_2d fp32 B=4 H=8 d=64 (64,64)x(128,128) scale_front forward (BASELINE config 5)",
     "d32": "full_1d fp16 B=8 H=16 d=32 Nq=Nk=4096 forward (config 2 at the reference tests' d=32; diagnostic)",
     "w256": "full_1d fp16 B=8 H=16 d=256 Nq=Nk=4096 forward (config 2 at d=256, past 128 channels; diagnostic)",
+    "w256b": "causal_1d fp16 B=8 H=16 d=256 N=8192 forward+backward (config 3 at d=256; diagnostic)",
 }
 DTYPE_NAME = {torch.float16: "fp16", torch.float32: "fp32", torch.float64: "fp64"}
 

@@ -816,6 +816,8 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2291: return launch_t<kFDefaultR2 | kFSumsF32>(a, s);
     case 2292: return launch_t<kFDefaultR2 | kFHalfMax>(a, s);
     case 2293: return launch_t<kFDefaultR2>(a, s);  // round-2 default (exact fp32 row max every tile)
+    case 2294: return launch_t<kFDefault | kANoSums>(a, s);            // timing only: no row sums (outputs wrong)
+    case 2295: return launch_t<kFDefault | kANoExp | kANoMax | kANoSums>(a, s);  // timing only: no softmax
     case 2297: return launch_t<kFDefault | kANoExp>(a, s);             // timing only: no exp2 (outputs wrong)
     case 2298: return launch_t<kFDefault | kANoLoad | kANoStore>(a, s);  // timing only: no staging
     case 2299: return launch_t<kFDefault | kFStamp>(a, s);

@@ -20,7 +20,7 @@ if [ "$1" == "--collect" ]; then   # local: keep the summaries, drop the raw tra
 fi
 export TMPDIR=/tmp
 mkdir -p $OUT
-declare -A REGEX=([c2]=fwd_f16 [c3]="fwd_f16|bwd_dkdv|bwd_dq|bwd_prep" [c4]=fwd_f16 [c5]=fwd_f32_kernel [d32]=fwd_f16 [w256]="fwd_f16|generic")
+declare -A REGEX=([c2]=fwd_f16 [c3]="fwd_f16|bwd_dkdv|bwd_dq|bwd_prep" [c4]=fwd_f16 [c5]=fwd_f32_kernel [d32]=fwd_f16 [w256]="fwd_f16|generic" [w256b]="fwd_f16|bwd_dkdv|bwd_dq|bwd_prep|generic")
 for cfg in ${CONFIGS:-c2}; do
   rx=${REGEX[$cfg]}
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$cfg -o run \
