@@ -10,7 +10,9 @@ outputs that vanish analytically, e.g. dQ when a row attends a single key):
   fp64: rtol 1e-10 / atol 1e-10*max
 l is checked with the same rtol (l for fp16 is fp32), m to two units in the last
 place of T (it is the rounded row max) — for fp16 plus rtol 1e-3 / atol 1e-3*max(|m|,1),
-since the fp16 kernel scores with Q pre-scaled by scale*log2(e) in fp16.  The reference's own gate
+since the fp16 kernel scores with Q pre-scaled by scale*log2(e) in fp16; for fp32 / fp64 plus
+1e-6*|m| and the larger of 1e-6 (1e-12) and 2 eps of the score's rounding bound scale*|q|_1*max|k|.
+The reference's own gate
 (rtol=atol=1e-3*N for fp16, 1e-6*N otherwise; tests/test_base.py:198-226) is far
 looser and is implied.  Rows that attend nothing must be exactly O=0, l=0,
 m=bytes 0xFA.
@@ -113,8 +115,17 @@ def run_case(dtype, policy, seq_dims, mode, batch, d, vd, qs, ks, ws=1, ls=0, ca
         ulp = np.abs(np.spacing(np.abs(M64[:, ha]).astype(dtype))).astype(np.float64)
         # m: 2 ulp of T, plus (fp16) the same rtol/atol-with-floor-1 as the other outputs — the
         # fp16 kernel forms its scores from Q pre-scaled by scale*log2(e) in fp16 (~1e-4 abs)
+        # fp32 / fp64: m is a score, a d-term dot product rounded in T (Q pre-scaled, then the MFMA's
+        # fma chain), so its absolute error scales with scale·Σ|q_c·k_c| <= scale·|q|_1·max|k|, not
+        # with |m| (a row max near 0 can come from large, cancelling terms); allow 2 units of T's
+        # rounding of that bound
+        eps = float(np.finfo(dtype).eps)
+        qn1 = np.abs(Qf[sl].astype(np.float64)).sum(axis=1).reshape(len(sl), nq)[:, ha]
+        kmax = max(float(np.abs(Kf[sl]).max()), 1e-30)
+        dot_bound = qn1 * kmax / math.sqrt(d)
         m_tol = 2 * ulp + (1e-3 * np.maximum(np.abs(M64[:, ha]), 1.0) if dtype == np.float16
-                           else 1e-6 * np.abs(M64[:, ha]) + (1e-6 if dtype != np.float64 else 1e-12))
+                           else 1e-6 * np.abs(M64[:, ha]) + np.maximum(1e-6 if dtype != np.float64 else 1e-12,
+                                                                      2 * eps * dot_bound))
         assert (np.abs(m_f - M64[:, ha]) <= m_tol).all(), f"m: max err {np.abs(m_f - M64[:, ha]).max():.3e}"
         l_ref = L64[:, ha] * np.exp(M64[:, ha] - m_f)    # relative to the stored m
         _close("l", lg[:, ha], l_ref, max(rtol, 1e-6 if dtype == np.float16 else rtol), atol)
@@ -318,6 +329,20 @@ def test_wide_channels(dtype, d, vd, policy, ws, causal):
 ])
 def test_wide_channels_mfma_forward(d, vd, policy, mode, qs, ks, ws, causal):
     run_case(np.float16, policy, 1, mode, (2,), d, vd, qs, ks, ws=ws, causal=causal, bwd=False, seed=d + 3 * vd)
+
+
+# fp32 forward for 128 < max(d, v_d) <= 256 on MFMA (fa_fwd_f32_wide.hip: 32-key tiles, every rule, any
+# alignment and length)
+@pytest.mark.parametrize("d,vd", [(256, 256), (160, 160), (130, 200), (200, 64), (64, 256)])
+@pytest.mark.parametrize("policy,seq,mode,qs,ks,ws,ls,causal", [
+    ("full", 1, "none_front", (300,), (517,), 1, 1, False),
+    ("causal", 1, "scale_end", (203,), (520,), 1, 1, False),
+    ("local", 1, "scale_front", (240,), (481,), 70, 1, True),
+    ("local", 2, "none_front", (13, 22), (13, 22), 5, 3, True),
+])
+def test_wide_channels_mfma_forward_f32(d, vd, policy, seq, mode, qs, ks, ws, ls, causal):
+    run_case(np.float32, policy, seq, mode, (2,), d, vd, qs, ks, ws=ws, ls=ls, causal=causal, bwd=False,
+             seed=d + 7 * vd)
 
 
 # fp16 backward for 128 < max(d, v_d) <= 256 on MFMA (fa_bwd_f16_fast.hip launch_bwd_wide: the one-wave

@@ -48,8 +48,14 @@ def test_shipped_library_has_no_store_hazard():
     import check_store_hazard as H
     lib = os.path.join(ROOT, "tf_flash_attention_amd", "libfa_hip.so")
     objs = H.disassemble_library(lib)
-    n_tu = sum("__global__" in open(p).read()  # translation units with kernels (fa_api.hip has none)
-               for p in glob.glob(os.path.join(ROOT, "tf_flash_attention_amd", "csrc", "*.hip")))
+    csrc = os.path.join(ROOT, "tf_flash_attention_amd", "csrc")
+
+    def has_kernels(p):  # the unit's own text or a shared kernel header it includes (*_impl.h)
+        text = open(p).read()
+        impl = [ln.split('"')[1] for ln in text.splitlines() if ln.startswith('#include "') and '_impl.h"' in ln]
+        return "__global__" in text + "".join(open(os.path.join(csrc, f)).read() for f in impl)
+    # translation units with kernels (fa_api.hip has none)
+    n_tu = sum(has_kernels(p) for p in glob.glob(os.path.join(csrc, "*.hip")))
     assert len(objs) == n_tu
     assert sum(d.count("buffer_store") + d.count("global_store") for _, d in objs) > 100
     found = []

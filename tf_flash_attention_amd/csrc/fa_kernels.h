@@ -81,6 +81,7 @@ bool bwd_f16_supported(const BwdArgs& a);
 // fp32 MFMA forward — fa_fwd_f32.hip
 bool fwd_f32_supported(const FwdArgs& a);
 hipError_t launch_fwd_f32(const FwdArgs& a, hipStream_t s);
+hipError_t launch_fwd_f32_wide(const FwdArgs& a, hipStream_t s);  // fa_fwd_f32_wide.hip (D = 256)
 // fp32 MFMA backward (two-pass) — fa_bwd_f32.hip
 bool bwd_f32_supported(const BwdArgs& a);
 hipError_t launch_bwd_f32(const BwdArgs& a, hipStream_t s);

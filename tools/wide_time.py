@@ -1,4 +1,4 @@
-"""Forward and backward time at 256 channels (config 2's shape at d = 256): the MFMA kernels
+"""Forward and backward time at 256 channels, plus the fp32 forward there (config 2's shape at d = 256): the MFMA kernels
 (fa_fwd_f16_wide.hip; fa_bwd_f16_fast.hip launch_bwd_wide) against the SIMT kernels the same calls took
 before round 4 (reached here through a K pointer one element off 16-B alignment, which the MFMA kernels
 do not take).  Usage: python tools/wide_time.py [b] [n]"""
@@ -58,6 +58,14 @@ def main():
     print(json.dumps({"shape": f"full_1d fp16 b={b} d={d} n={n}", "pass": "backward", "mfma_ms": round(t_bm, 4),
                       "mfma_tflops": round(bflops / t_bm / 1e9, 1), "simt_ms": round(t_bs, 4),
                       "simt_tflops": round(bflops / t_bs / 1e9, 1), "max_rel_diff": diff}), flush=True)
+    # fp32 forward on the MFMA kernel (fa_fwd_f32_wide.hip), a quarter of the batch
+    b32 = max(b // 4, 1)
+    q32, k32, v32 = (x[:b32].float() for x in (q, k, v))
+    t32 = timed(lambda: fa.attention_forward("full", 1, q32, k32, v32, "none_front", 1, 0, False))
+    f32 = flops * b32 / b
+    print(json.dumps({"shape": f"full_1d fp32 b={b32} d={d} n={n}", "pass": "forward", "mfma_ms": round(t32, 4),
+                      "mfma_tflops": round(f32 / t32 / 1e9, 1), "fp32_mfma_peak_frac": round(f32 / t32 / 1e9 / 157.3, 3)}),
+          flush=True)
 
 
 if __name__ == "__main__":
