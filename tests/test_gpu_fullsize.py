@@ -7,7 +7,12 @@ sampled slices are copied back and checked against the float64 oracle with the t
 tests/test_gpu_parity.py (first, middle and last slices, plus the slices where the XCD ranges
 and persistent workgroups of the band kernel change hands).
 
-Size-independent properties cover the slices the oracle does not see:
+Every slice (round 4): the same float64 math as the oracle, evaluated on the GPU over the whole
+batch (_batch_ref_f64: the oracle's own rule evaluator supplies each row block's column band and
+mask, torch does the float64 products), is checked against the numpy oracle on the sampled slices
+to 1e-9 and then stands in for it on all of them, with the same tolerances.
+
+Size-independent properties over the whole batch as well:
   * batch reversal: the op on the batch in reverse slice order is bitwise the reverse of the
     op on the batch.  A slice's result then does not depend on which workgroup, XCD or
     persistent item walked it, so one wrong walk step anywhere in the batch shows up;
@@ -56,6 +61,80 @@ def _check_lm(dtype, lg, mg, L64, M64, ha):
     _close("l", lg[:, ha].astype(np.float64), l_ref, max(rtol, 1e-6 if dtype == np.float16 else rtol), atol)
 
 
+def _batch_ref_f64(q, k, v, do, prob, q_seq, k_seq, bchunk):
+    """O, l, m (and dQ, dK, dV when do is given) of every slice in float64 on the GPU: the numpy
+    oracle's formulas (oracle/fa_oracle.py forward_f64 / backward_f64, row chunks with the rule's
+    column band and mask from its own evaluator), batched over slices.  q, k, v, do: [b, c, n]."""
+    b, d, nq = q.shape
+    vd, nk = v.shape[1], k.shape[2]
+    dev = q.device
+    scale = 1.0 / np.sqrt(d)
+    Of = torch.zeros((b, vd, nq), dtype=torch.float64, device=dev)
+    Mf = torch.zeros((b, nq), dtype=torch.float64, device=dev)
+    Lf = torch.zeros((b, nq), dtype=torch.float64, device=dev)
+    grads = None
+    if do is not None:
+        grads = tuple(torch.zeros((b, c, n), dtype=torch.float64, device=dev) for c, n in ((d, nq), (d, nk), (vd, nk)))
+    ha_all = np.zeros(nq, dtype=bool)
+    for r0, r1, c0, c1, mk in O._row_chunks(O._evaluator(prob, q_seq, k_seq), nq):
+        if c1 == c0:
+            continue
+        ha = mk.any(axis=1)
+        ha_all[r0:r1] = ha
+        mk_t = torch.from_numpy(mk).to(dev)
+        ha_t = torch.from_numpy(ha).to(dev)
+        for b0 in range(0, b, bchunk):
+            b1 = min(b, b0 + bchunk)
+            qi = q[b0:b1, :, r0:r1].double()
+            ki = k[b0:b1, :, c0:c1].double()
+            vi = v[b0:b1, :, c0:c1].double()
+            s = torch.where(mk_t, torch.matmul(qi.transpose(1, 2), ki) * scale, -torch.inf)
+            mrow = torch.where(ha_t, s.amax(dim=2), 0.0)
+            p = torch.exp(s - mrow[:, :, None])
+            lsum = p.sum(dim=2)
+            p = p / torch.where(ha_t, lsum, 1.0)[:, :, None]
+            o = torch.matmul(vi, p.transpose(1, 2))
+            Of[b0:b1, :, r0:r1] = o
+            Mf[b0:b1, r0:r1] = mrow
+            Lf[b0:b1, r0:r1] = lsum
+            if grads is not None:
+                doi = do[b0:b1, :, r0:r1].double()
+                dQ, dK, dV = grads
+                dV[b0:b1, :, c0:c1] += torch.matmul(doi, p)
+                dp = torch.matmul(doi.transpose(1, 2), vi)
+                D = (doi * o).sum(dim=1)
+                ds = p * (dp - D[:, :, None]) * scale
+                dQ[b0:b1, :, r0:r1] = torch.matmul(ki, ds.transpose(1, 2))
+                dK[b0:b1, :, c0:c1] += torch.matmul(qi, ds)
+            del s, p
+    return Of, Lf, Mf, ha_all, grads
+
+
+def _close_gpu(name, got, ref, rtol, atol_rel):
+    """tests/test_gpu_parity._close on device tensors (per slice scale: max(max|ref|, 1) over the batch)."""
+    got = got.double()
+    scale = max(float(ref.abs().max()), 1.0)
+    err = (got - ref).abs()
+    bad = err > atol_rel * scale + rtol * ref.abs()
+    assert bool(torch.isfinite(got).all()), f"{name}: non-finite output"
+    nbad = int(bad.sum())
+    assert nbad == 0, f"{name}: {nbad} / {bad.numel()} elements off (whole batch); max abs err {float(err.max()):.3e}"
+
+
+def _check_lm_gpu(dtype, lg, mg, L64, M64, ha):
+    rtol, atol = TOL[dtype]["fwd"]
+    h = torch.from_numpy(ha).to(lg.device)
+    m_f = mg.double()[:, h]
+    Mr = M64[:, h]
+    _, ex = torch.frexp(Mr.abs())  # ulp of |m| in T: 2^(e - 1 - mantissa bits)
+    ulp = torch.ldexp(torch.ones_like(Mr), ex - 1 - (10 if dtype == np.float16 else 23))
+    m_tol = 2 * ulp + (1e-3 * torch.clamp(Mr.abs(), min=1.0) if dtype == np.float16 else 1e-6 * Mr.abs() + 1e-6)
+    err = (m_f - Mr).abs()
+    assert bool((err <= m_tol).all()), f"m: max err {float(err.max()):.3e} (whole batch)"
+    _close_gpu("l", lg.double()[:, h], L64[:, h] * torch.exp(Mr - m_f), max(rtol, 1e-6 if dtype == np.float16 else rtol),
+               atol)
+
+
 def _properties(o, l, v, name):
     vmax = float(v.abs().max())
     assert bool(torch.isfinite(o).all()), f"{name}: non-finite O"
@@ -65,7 +144,7 @@ def _properties(o, l, v, name):
 
 
 def run_full_size(dtype, policy, seq_dims, mode, batch, d, qs, ks, ws=1, bwd=False, slices=(), seed=0,
-                  reverse=True):
+                  reverse=True, bchunk=16):
     fa = _fa()
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev).manual_seed(seed)
@@ -99,6 +178,33 @@ def run_full_size(dtype, policy, seq_dims, mode, batch, d, qs, ks, ws=1, bwd=Fal
         _close("dQ", flat(q.grad, d)[sl].cpu().numpy(), dQ.reshape(len(sl), d, nq), rtol, atol)
         _close("dK", flat(k.grad, d)[sl].cpu().numpy(), dK.reshape(len(sl), d, nk), rtol, atol)
         _close("dV", flat(v.grad, d)[sl].cpu().numpy(), dV.reshape(len(sl), d, nk), rtol, atol)
+    # ---- every slice: the oracle's float64 math on the GPU, pinned to the numpy oracle on the
+    #      sampled slices, then checked against the op over the whole batch
+    Rf = _batch_ref_f64(flat(q, d), flat(k, d), flat(v, d), flat(do, d) if bwd else None, prob, tuple(qs), tuple(ks),
+                        bchunk)
+    RO, RL, RM, rha, rgrads = Rf
+    assert (rha == ha).all()
+    sl_t = torch.tensor(sl, device=dev)
+    pin = [("O", RO, O64.reshape(len(sl), d, nq)), ("l", RL, L64.reshape(len(sl), nq)),
+           ("m", RM, M64.reshape(len(sl), nq))]
+    if bwd:
+        pin += [("dQ", rgrads[0], dQ.reshape(len(sl), d, nq)), ("dK", rgrads[1], dK.reshape(len(sl), d, nk)),
+                ("dV", rgrads[2], dV.reshape(len(sl), d, nk))]
+    for name, r, o64 in pin:
+        got, want = r.index_select(0, sl_t).cpu().numpy(), np.asarray(o64, dtype=np.float64)
+        fin = np.isfinite(want)
+        assert (np.isfinite(got) == fin).all(), f"batch reference {name}: finiteness differs from the oracle"
+        assert np.abs(got[fin] - want[fin]).max() <= 1e-9 * max(np.abs(want[fin]).max(), 1.0), \
+            f"batch reference {name} disagrees with the numpy oracle"
+    rtol, atol = TOL[dtype]["fwd"]
+    _close_gpu("O", flat(o, d), RO, rtol, atol)
+    _check_lm_gpu(dtype, flat(l, 0), flat(m, 0), RL, RM, ha)
+    if bwd:
+        rtol, atol = TOL[dtype]["bwd"]
+        for name, g, r in (("dQ", q.grad, rgrads[0]), ("dK", k.grad, rgrads[1]), ("dV", v.grad, rgrads[2])):
+            _close_gpu(name, flat(g, d), r, rtol, atol)
+    del Rf, RO, RL, RM, rgrads
+    torch.cuda.empty_cache()
     # ---- size-independent properties over the whole batch
     if ha.all():
         _properties(o.detach(), l, v.detach(), "batch")
@@ -121,13 +227,13 @@ def run_full_size(dtype, policy, seq_dims, mode, batch, d, qs, ks, ws=1, bwd=Fal
 def test_config2_full_size():
     """Config 2: full_1d fp16 B=8 H=16 d=64 N=4096, forward (the headline kernel)."""
     run_full_size(np.float16, "full", 1, "none_front", (8, 16), 64, (4096,), (4096,), slices=(0, 31, 64, 127),
-                  seed=2)
+                  seed=2, bchunk=64)
 
 
 def test_config3_full_size():
     """Config 3: causal_1d fp16 B=8 H=16 d=128 N=8192, forward + backward."""
     run_full_size(np.float16, "causal", 1, "none_front", (8, 16), 128, (8192,), (8192,), bwd=True,
-                  slices=(0, 63, 127), seed=3)
+                  slices=(0, 63, 127), seed=3, bchunk=32)
 
 
 def test_config4_full_size():
@@ -135,7 +241,7 @@ def test_config4_full_size():
     65,536 persistent items).  The band kernel deals one eighth of the items to each XCD and
     every J-th of those to a workgroup: slices 127/128, 511/512 and 895/896 straddle XCD ranges."""
     run_full_size(np.float16, "local", 1, "none_front", (64, 16), 64, (16384,), (16384,), ws=256,
-                  slices=(0, 1, 127, 128, 511, 512, 895, 896, 1023), seed=4)
+                  slices=(0, 1, 127, 128, 511, 512, 895, 896, 1023), seed=4, bchunk=128)
 
 
 def test_config4_per_gpu_shard():
@@ -144,7 +250,7 @@ def test_config4_per_gpu_shard():
     s0, s1 = shard.shard_range(1024, 8, 3)
     assert s1 - s0 == 128
     run_full_size(np.float16, "local", 1, "none_front", (s1 - s0,), 64, (16384,), (16384,), ws=256,
-                  slices=(0, 15, 16, 63, 64, 127), seed=40 + s0)
+                  slices=(0, 15, 16, 63, 64, 127), seed=40 + s0, bchunk=128)
 
 
 def test_config5_full_size():

@@ -60,6 +60,11 @@ constexpr int kFDot2 = 8;        // row sums of the fp16 P by v_dot2_f32_f16 (ha
 constexpr int kFHoistV = 2;      // read all V fragments before the PV MFMAs
 constexpr int kFOcc1 = 16;       // one wave per SIMD: the whole 512-entry register file
 constexpr int kFSched = 32;      // force a 1-MFMA/5-VALU interleave (sched_group_barrier)
+// row sums on the matrix pipe: one more MFMA per PV k-step with an all-ones A operand (every row of
+// its accumulator is the query's running sum), instead of v_dot2c on the VALU.  At d <= 32 a tile's
+// 8 MFMAs leave the pipe idle two thirds of the time beside the softmax issue, so the 4 extra
+// MFMAs are free and the 16 dot2c they replace are not
+constexpr int kFMfmaSum = 64;
 
 template <int D, int NW>
 struct Smem {
@@ -253,6 +258,10 @@ __global__ __launch_bounds__(NW * 64, waves_per_eu(D, F)) void fwd_f16_kernel(Fw
   // to; negm = -m_run broadcast (the C operand of every Sᵀ chain); m_max: exact row max.
   float m_run = 0.f, l_run = 0.f, m_max = kNegInf;
   bool m_set = false;
+  constexpr bool MSUM = (F & kFMfmaSum) != 0;
+  floatx16 acc_l;  // MSUM: the running row sum in every register (rows are identical)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc_l[i] = 0.f;
   floatx16 negm;
 #pragma unroll
   for (int i = 0; i < 16; ++i) negm[i] = 0.f;
@@ -319,6 +328,10 @@ __global__ __launch_bounds__(NW * 64, waves_per_eu(D, F)) void fwd_f16_kernel(Fw
       m_run += delta;
       m_set = m_set || seed;
       l_run *= alpha;
+      if constexpr (MSUM) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc_l[i] *= alpha;
+      }
 #pragma unroll
       for (int u = 0; u < D / 32; ++u)
 #pragma unroll
@@ -351,7 +364,12 @@ __global__ __launch_bounds__(NW * 64, waves_per_eu(D, F)) void fwd_f16_kernel(Fw
       half8 pf;
 #pragma unroll
       for (int j = 0; j < 8; ++j) pf[j] = (_Float16)__builtin_amdgcn_exp2f(st[s >> 1][8 * (s & 1) + j]);
-      if (F & kFDot2) {
+      if constexpr (MSUM) {
+        half8 ones;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ones[j] = (_Float16)1.f;
+        acc_l = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones, pf, acc_l, 0, 0, 0);
+      } else if (F & kFDot2) {
 #pragma unroll
         for (int j = 0; j < 8; j += 4) {
           ls0 = __builtin_amdgcn_fdot2(half2v{pf[j], pf[j + 1]}, one2, ls0, false);
@@ -419,7 +437,7 @@ __global__ __launch_bounds__(NW * 64, waves_per_eu(D, F)) void fwd_f16_kernel(Fw
   }
 
   if (!wave_active) return;
-  const float l_tot = l_run + xor32(l_run);
+  const float l_tot = MSUM ? acc_l[0] : l_run + xor32(l_run);
   const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
   if (qi < nq) {
     __half* O = static_cast<__half*>(a.O) + bi * (int64_t)vd * nq;
@@ -477,6 +495,12 @@ hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s) {
 #ifdef FA_DIAG
   // FA_FWD_VARIANT = <NW><F> below 1000 pins this general kernel (A/B runs), e.g. 408
   const int v = diag_variant("FA_FWD_VARIANT");
+  if (v >= 0 && v < 1000 && dm <= 32) {  // d <= 32: 308 dot2c row sums (the round-3 default), 372 MFMA row sums
+    if (v == 308) return launch_t<32, 4, 8>(a, s);
+    if (v == 372) return launch_t<32, 4, 8 | kFMfmaSum>(a, s);
+    if (v == 808) return launch_t<32, 8, 8>(a, s);
+    if (v == 872) return launch_t<32, 8, 8 | kFMfmaSum>(a, s);
+  }
   if (v >= 0 && v < 1000 && dm > 32 && dm <= 64) {
     switch (v) {
       case 400: return launch_t<64, 4, 0>(a, s);
