@@ -345,6 +345,19 @@ def test_wide_channels_mfma_forward_f32(d, vd, policy, seq, mode, qs, ks, ws, ls
              seed=d + 7 * vd)
 
 
+# fp32 backward for 128 < max(d, v_d) <= 256 on MFMA (fa_bwd_f32_wide.hip: 16x16x4 MFMAs, 16 keys /
+# queries a wave; every rule, any alignment and length)
+@pytest.mark.parametrize("d,vd", [(256, 256), (160, 160), (130, 200), (200, 64), (64, 256)])
+@pytest.mark.parametrize("policy,seq,mode,qs,ks,ws,ls,causal", [
+    ("full", 1, "none_front", (131,), (197,), 1, 1, False),
+    ("causal", 1, "scale_end", (150,), (75,), 1, 1, False),
+    ("local", 1, "scale_front", (120,), (241,), 40, 1, True),
+    ("local", 2, "none_front", (9, 14), (9, 14), 4, 2, True),
+])
+def test_wide_channels_mfma_backward_f32(d, vd, policy, seq, mode, qs, ks, ws, ls, causal):
+    run_case(np.float32, policy, seq, mode, (2,), d, vd, qs, ks, ws=ws, ls=ls, causal=causal, seed=d + 11 * vd)
+
+
 # fp16 backward for 128 < max(d, v_d) <= 256 on MFMA (fa_bwd_f16_fast.hip launch_bwd_wide: the one-wave
 # dK / dV and dQ passes at D = 256, two 128-channel output chunks per slice; aligned tensors, lengths
 # multiples of 8, every rule incl. 2-D windows)

@@ -1,7 +1,7 @@
 // fa_bwd_f32.hip — fp32 fused attention backward on gfx950 MFMA (v_mfma_f32_32x32x2_f32).
 //
 // Replaces the reference's BackwardImpl (flash_attention.cu:1079-1967) for fp32
-// inputs (any d, v_d <= 128, every policy / sync mode / rule).  The f32-input MFMA
+// inputs (any d, v_d <= 128, every policy / sync mode / rule; up to 256 in fa_bwd_f32_wide.hip).  The f32-input MFMA
 // is a k-ordered fmaf chain at the f32 vector rate, so numerics stay full fp32
 // (the 1e-5 parity target) while the five GEMMs of the backward leave the VALU.
 // Same two-pass split as the fp16 backward (fa_bwd_f16_fast.hip), no atomics:
@@ -419,8 +419,9 @@ hipError_t launch_t(const BwdArgs& a, hipStream_t s) {
 }  // namespace
 
 bool bwd_f32_supported(const BwdArgs& a) {
-  return a.d >= 1 && a.v_d >= 1 && a.d <= 128 && a.v_d <= 128 &&
-         a.b * ((a.rule.k.n + 127) / 128) < (1ll << 31) && a.b * ((a.rule.q.n + 127) / 128) < (1ll << 31);
+  // (128 < max(d, v_d) <= 256: fa_bwd_f32_wide.hip, 64-key / 64-query workgroups)
+  return a.d >= 1 && a.v_d >= 1 && a.d <= 256 && a.v_d <= 256 &&
+         a.b * ((a.rule.k.n + 63) / 64) < (1ll << 31) && a.b * ((a.rule.q.n + 63) / 64) < (1ll << 31);
 }
 
 hipError_t launch_bwd_f32(const BwdArgs& a, hipStream_t s) {
@@ -432,7 +433,8 @@ hipError_t launch_bwd_f32(const BwdArgs& a, hipStream_t s) {
   const int dm = max(a.d, a.v_d);
   if (dm <= 32) return launch_t<32>(a, s);
   if (dm <= 64) return launch_t<64>(a, s);
-  return launch_t<128>(a, s);
+  if (dm <= 128) return launch_t<128>(a, s);
+  return launch_bwd_f32_wide(a, s);
 }
 
 }  // namespace fa

@@ -65,6 +65,14 @@ constexpr int kANoExp = 8, kANoMax = 16, kANoSums = 32;
 constexpr int kANoLoad = 64, kANoStore = 128, kANoFrag = 256;
 // staging by LDS-DMA (buffer_load ... lds straight into the ring, no VGPR round trip / ds_write)
 constexpr int kFDma = 512;
+// (with kFDma) the LDS-DMA issued by inline assembly: hipcc does not see an LDS write, so it adds no
+// vmcnt(0) before the later fragment reads (it does for its own LDS-DMA builtin, which it cannot
+// prove disjoint from them); the waits are the explicit vmcnt(6) before each barrier
+constexpr int kFDmaAsm = 1 << 23;
+// row sums on the matrix pipe: one v_mfma_f32_16x16x32_f16 per PV k-step in the MFMA phase, its A
+// operand a 0/1 selector (row 0 sums the P columns of queries 0-15, row 1 those of 16-31), instead
+// of 16 v_dot2c in the softmax phase; lanes 0-15 hold the running sums of queries c and 16 + c
+constexpr int kFSumsMfma = 1 << 24;
 // diagnostic: workgroup timeline (s_memrealtime at entry / after the prologue / after the loop /
 // at exit, cycle counts, HW_ID, XCC_ID) written as raw words over the block's first l entries
 constexpr int kFStampWG = 2048;
@@ -156,8 +164,18 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   const uint32_t vdoff = drow < vd ? (uint32_t)drow * (uint32_t)nk * 2u + 16u * vcm : 0x80000000u;
   auto dma = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, int cmx, int k0, int lds_off) __attribute__((always_inline)) {
     const bool in = k0 + 8 * cmx < nk;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + lds_off + 1024 * w), 16,
-                                             in ? off : 0x80000000u, 2 * min(k0, nk), 0, 0);
+    if constexpr ((F & kFDmaAsm) != 0) {
+      // M0 = the wave's LDS destination (lane L writes its 16 B at M0 + 16 L)
+      const uint32_t m0v = (uint32_t)(uintptr_t)(smem + lds_off) + 1024u * (uint32_t)w;
+      // (s_nop 0: the one wait state between the SALU write of M0 and an LDS-DMA that reads it)
+      asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+                   :
+                   : "v"(in ? off : 0x80000000u), "s"(rs), "s"(2 * min(k0, nk)), "{m0}"(m0v)
+                   : "memory");
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + lds_off + 1024 * w),
+                                               16, in ? off : 0x80000000u, 2 * min(k0, nk), 0, 0);
+    }
   };
 
   u32x4 kst[3], vst[3];
@@ -275,7 +293,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
 
   half8 kf[2][4];  // K fragments for the next Sᵀ
   half8 vf[4][2];  // V fragments for the next PV
-  constexpr bool ILV = (F & kFInterleave) != 0 && POL == 0 && !DMA;
+  // (the builtin LDS-DMA's vmcnt(0) before every fragment read defeats the interleave; the inline-asm
+  // DMA has none)
+  constexpr bool ILV = (F & kFInterleave) != 0 && POL == 0 && (!DMA || (F & kFDmaAsm) != 0);
   if constexpr (ILV) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -337,6 +357,15 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
       }
   };
   float lacc[4] = {0.f, 0.f, 0.f, 0.f};  // kFSumsAcc: running row sums (chains x = 0..3)
+  constexpr bool MSUM = (F & kFSumsMfma) != 0;
+  floatx4 lsum = {0.f, 0.f, 0.f, 0.f};     // MSUM: lane c < 16: [0] query c, [1] query 16 + c
+  half8 lsel;                               // MSUM: selector row (lane & 15) over k = 8 (lane >> 4) + j
+  {
+    const int srow = lane & 15, sg = (lane >> 4) & 1;
+    const _Float16 sv = (_Float16)(((srow == 0 && sg == 0) || (srow == 1 && sg == 1)) ? 1.f : 0.f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lsel[j] = sv;
+  }
   float ts[4];                            // kFSumsF32: this tile's row sums (four chains)
   auto row_sums = [&]() __attribute__((always_inline)) {
     const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
@@ -427,6 +456,11 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
 #pragma unroll
         for (int x = 0; x < 4; ++x) lacc[x] *= alpha;
       }
+      if constexpr (MSUM) {  // lane c's [1] holds query 16 + c: that lane's factor
+        const float ahi = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * ((lane & 15) + 16), __float_as_int(alpha)));
+        lsum[0] *= alpha;
+        lsum[1] *= ahi;
+      }
       l0 *= alpha;
       l1 *= alpha;
 #pragma unroll
@@ -440,7 +474,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
       exp_cvt();
       pmr = half2v{(_Float16)0.f, (_Float16)0.f};
     }
-    if (!(F & (kFSumsLate | kANoSums))) row_sums();
+    if (!(F & (kFSumsLate | kANoSums | kFSumsMfma))) row_sums();
   };
   auto softmax = [&](int it, int cls) __attribute__((always_inline)) {
     if constexpr (PMAX) {
@@ -489,7 +523,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
       }
       exp_cvt();
     }
-    if (!(F & (kFSumsLate | kANoSums))) row_sums();
+    if (!(F & (kFSumsLate | kANoSums | kFSumsMfma))) row_sums();
   };
 
   // MFMA(i): this wave's chunks of K(i+3) / V(i+2) into LDS (over K(i) / V(i-1), whose
@@ -534,6 +568,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         const half8 p = __builtin_bit_cast(half8, u32x4{pw[s][0], pw[s][1], pw[s][2], pw[s][3]});
 #pragma unroll
         for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[u], 0, 0, 0);
+        if constexpr (MSUM) lsum = __builtin_amdgcn_mfma_f32_16x16x32_f16(lsel, p, lsum, 0, 0, 0);
 #pragma unroll
         for (int u = 0; u < 2; ++u)
           if (!(F & kANoFrag)) vf[s][u] = read_b128(pv + vbase[s] + 32 * u * 128);
@@ -562,7 +597,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, MSUM ? 3 : 2, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
           if constexpr ((F & kFIlvStores) != 0) {
             if (s == kIlvAt) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
@@ -586,6 +621,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         const half8 p = __builtin_bit_cast(half8, u32x4{pw[s][0], pw[s][1], pw[s][2], pw[s][3]});
 #pragma unroll
         for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, o[u], 0, 0, 0);
+        if constexpr (MSUM) lsum = __builtin_amdgcn_mfma_f32_16x16x32_f16(lsel, p, lsum, 0, 0, 0);
       }
     }
     if (!ILV && !(F & kANoFrag)) read_v(c);
@@ -682,7 +718,15 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   if constexpr ((F & kFHalfMax) != 0) m_max = max_pair32(m_max);
   if constexpr (PMAX)
     m_max = max_pair32(fmaxf(m_max, m_run + __log2f((float)__builtin_elementwise_maximum(pmr[0], pmr[1]))));
-  const float l_tot = sum_pair32(l0 + l1);
+  float l_tot;
+  if constexpr (MSUM) {  // query q = lane & 31 sits in lane q & 15, register q >> 4
+    const int src = 4 * (lane & 15);
+    const float s0 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(lsum[0])));
+    const float s1 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(lsum[1])));
+    l_tot = (r < 16) ? s0 : s1;
+  } else {
+    l_tot = sum_pair32(l0 + l1);
+  }
   const float inv = (l_tot > 0.f) ? 1.f / l_tot : 0.f;
   if (qi >= nq) return;
   __half* O = static_cast<__half*>(a.O) + bi * (int64_t)vd * nq;
@@ -800,6 +844,13 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2279: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores | kFStampWG | kANoExp | kANoMax | kANoSums>(a, s);
     case 2280: return launch_t<kFPrio | kFStoresLate | kFInterleave | kFIlvStores | kFStampWG | kANoLoad | kANoStore | kANoFrag | kANoExp | kANoMax | kANoSums>(a, s);
     case 2212: return launch_t<kFPrio | kFDma>(a, s);
+    case 2217: return launch_t<kFPrio | kFDma | kFDmaAsm>(a, s);
+    case 2218: return launch_t<kFPrio | kFDma | kFDmaAsm | kFSumsAcc | kFPMax>(a, s);
+    case 2230: return launch_t<kFDefault | kFDma | kFDmaAsm>(a, s);
+    case 2233: return launch_t<kFDefault | kFSumsMfma>(a, s);
+    case 2234: return launch_t<kFDefault | kFDma | kFDmaAsm | kFSumsMfma>(a, s);
+    case 2231: return launch_t<(kFDefault & ~kFIlvStores) | kFDma | kFDmaAsm>(a, s);
+    case 2232: return launch_t<(kFDefault & ~kFIlvStores) | kFDma | kFDmaAsm | kFIlvFine>(a, s);
     case 2205: return launch_t<kFPrio | kFSumsLate>(a, s);
     case 2211: return launch_t<kFPrio | kFStamp | kANoExp>(a, s);
     case 2219: return launch_t<kFPrio | kFStamp | kANoMax>(a, s);

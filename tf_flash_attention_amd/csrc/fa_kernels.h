@@ -85,8 +85,9 @@ hipError_t launch_fwd_f32_wide(const FwdArgs& a, hipStream_t s);  // fa_fwd_f32_
 // fp32 MFMA backward (two-pass) — fa_bwd_f32.hip
 bool bwd_f32_supported(const BwdArgs& a);
 hipError_t launch_bwd_f32(const BwdArgs& a, hipStream_t s);
+hipError_t launch_bwd_f32_wide(const BwdArgs& a, hipStream_t s);  // fa_bwd_f32_wide.hip (D = 256, after the prep)
 hipError_t launch_bwd_f16(const BwdArgs& a, hipStream_t s);
-// fp64 MFMA forward (d, v_d <= 128) and two-pass backward (d, v_d <= 64) — fa_f64.hip
+// fp64 MFMA forward and two-pass backward (d, v_d <= 128) — fa_f64.hip
 bool fwd_f64_supported(const FwdArgs& a);
 hipError_t launch_fwd_f64(const FwdArgs& a, hipStream_t s);
 bool bwd_f64_supported(const BwdArgs& a);

@@ -66,6 +66,13 @@ def main():
     print(json.dumps({"shape": f"full_1d fp32 b={b32} d={d} n={n}", "pass": "forward", "mfma_ms": round(t32, 4),
                       "mfma_tflops": round(f32 / t32 / 1e9, 1), "fp32_mfma_peak_frac": round(f32 / t32 / 1e9 / 157.3, 3)}),
           flush=True)
+    # fp32 backward (fa_bwd_f32_wide.hip)
+    o32, l32, m32 = fa.attention_forward("full", 1, q32, k32, v32, "none_front", 1, 0, False)
+    do32 = do[:b32].float()
+    tb32 = timed(lambda: fa.attention_backward("full", 1, q32, k32, v32, o32, l32, m32, do32, "none_front"))
+    print(json.dumps({"shape": f"full_1d fp32 b={b32} d={d} n={n}", "pass": "backward", "mfma_ms": round(tb32, 4),
+                      "mfma_tflops": round(2.5 * f32 / tb32 / 1e9, 1),
+                      "fp32_mfma_peak_frac": round(2.5 * f32 / tb32 / 1e9 / 157.3, 3)}), flush=True)
 
 
 if __name__ == "__main__":
