@@ -301,6 +301,29 @@ def test_band_forward_persistent(batch, nq, nk, ws, causal, mode, d):
              slices=sorted({0, 1, b // 3, b // 2 + 1, b - 2, b - 1}))
 
 
+@pytest.mark.parametrize("causal,ws", [(False, 100), (True, 77)])
+def test_band_edge_mask_large_scores(causal, ws):
+    """The band kernel's arithmetic edge mask (fa_fwd_f16_band.hip: min(s, ±(..)·2^100), rows never
+    seeded below -2^98) with scores near -3.7e5 in log2 units, past the round-3 constants (2^20 /
+    -2^18), where a row whose allowed scores all sat below the floor came back as O = 0.  Q and K are
+    constant, so every allowed score is the same and O is the mean of V over each row's window for
+    any rounding; m overflows fp16 there (as the reference's would), so only O is compared."""
+    fa = _fa()
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(7 + ws)
+    b, d, n = 3, 64, 1024
+    Q = np.full((b, d, n), 180.0, np.float16)
+    K = np.full((b, d, n), -180.0, np.float16)
+    V = rng.uniform(-2, 2, (b, d, n)).astype(np.float16)
+    o, l, m = fa.local_1d(*(torch.from_numpy(x).to(dev) for x in (Q, K, V)), ws, 0, causal, "none_front",
+                          returning_l_m=True)
+    torch.cuda.synchronize()
+    prob = O.Problem("local", 1, "none_front", ws, 0, causal)
+    O64, _, _, ha = O.forward_f64(Q, K, V, prob)
+    assert ha.all()
+    _close("O", o.cpu().numpy(), O64, *TOL[np.float16]["fwd"])
+
+
 @pytest.mark.parametrize("d,vd", [(64, 32), (24, 64), (100, 100), (7, 3)])
 def test_odd_channels(d, vd):
     for dt in DTYPES:

@@ -411,8 +411,8 @@ struct PcSmem {
   static constexpr int kBK = 128;            // keys per workgroup: four producer waves x 32
   static constexpr int kRow = D * kBK * 2;   // K (or V) row image (prologue only)
   static constexpr int kQT = D * 64;         // one [D][32] Q16 image
-  static constexpr int offQT = 0, offOT = kQT, offLse = 2 * kQT;
-  static constexpr int kSlot = offLse + 2 * 32 * 4;  // + -lse2[32], -D[32]
+  static constexpr int offQT = 0, offOT = kQT, offLse = 2 * kQT, offD = offLse + 256;
+  static constexpr int kSlot = offLse + 2 * 64 * 4;  // + -lse2[32], -D[32] (64-float vectors: LDS-DMA lanes)
   static constexpr int kNS = 4;              // query-tile ring
   static constexpr int offX = kNS * kSlot;   // P / dS hand-over: 2 slots x 4 waves x 4 KB
   static constexpr int kXWave = 4096;
@@ -434,6 +434,11 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   // PF & 4 (diagnostic build): per-wave s_memtime sums of each step's parts (stage + barrier, MFMA
   // part, softmax / hand-over part) written to the unused dQ workspace
   constexpr bool STAMP = (PF & 4) != 0;
+  // PF & 8: the query tiles staged by the consumer waves alone, as LDS-DMA issued by inline assembly
+  // (tile it+2 into the free ring slot at step it; hand-counted vmcnt before each barrier), so the
+  // producers, the step's critical path, carry no staging at all (16-B aligned shapes, D = 128)
+  constexpr bool DMA = (PF & 8) != 0 && ALN;
+  static_assert(!DMA || D == 128, "the LDS-DMA staging assumes 16 1-KB blocks a tile, four a consumer wave");
   uint64_t stv[3] = {0, 0, 0}, st_prev = 0;
   auto stamp = [&](int k) __attribute__((always_inline)) {
     if constexpr (STAMP) {
@@ -568,7 +573,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       const bool isO = is_o(j);
       *reinterpret_cast<lds_u32x4_t*>(base + (isO ? S::offOT : S::offQT) + q16_off(crow_[j], cm_[j])) = qr[set][j];
     }
-    if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr[set];
+    if (tid < 64) reinterpret_cast<lds_f_t*>(base + (tid < 32 ? S::offLse : S::offD - 128))[tid] = lr[set];
   };
   // hand-over slot of this wave pair: four b128 per lane (P k-steps 0/1, dS k-steps 0/1), lane-linear
   auto xoff = [&](int xs, int j) -> uint32_t { return S::offX + xs * S::kXSlot + wl * S::kXWave + j * 1024 + lane * 16; };
@@ -578,16 +583,75 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   // compile-time); loads and stores are unconditional (phantom tiles move zeros), so hipcc's vmcnt
   // waits stay exact.
   const int nsteps = ntiles + 1;
+  // ---- DMA staging (PF & 8): consumer wave wl issues the 1-KB blocks 4wl .. 4wl+3 of a tile (0-7 the
+  // Q16 image, 8-15 the dO16 image; block b = channel rows 16b .. 16b+15, lane L the 16 B at 16L =
+  // row 16b + L/4, position L%4, i.e. source chunk (L%4) ^ swizzle(row)); wave 4 also moves the row
+  // constants, -lse2 and -D of queries qa .. qa+63 by two dword LDS-DMAs (the first 32 used).  Past
+  // nq they read 0, not -inf / 0: those queries' Q and dO are zero too, so S = dP = D = 0, P = 1 and
+  // their dV / dK terms (dO·P, Q·dS with dS = P·(dP - D)) vanish all the same.
+  uint32_t dvoff[4];
+  int dcm[4];
+  const __amdgpu_buffer_rsrc_t lrs = make_rsrc(glse, 4u * nq), drs = make_rsrc(gD, 4u * nq);
+  if constexpr (DMA) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int blk = 4 * wl + j, b = blk & 7, row = 16 * b + (lane >> 2);
+      dcm[j] = (lane & 3) ^ ((row >> 2) & 3);
+      dvoff[j] = row < (blk >= 8 ? vd : d) ? (uint32_t)row * (uint32_t)nq * 2u + 16u * dcm[j] : 0x80000000u;
+    }
+  }
+  auto dma_tile = [&](int qa, int slot) __attribute__((always_inline)) {
+    if (wl == 0) {
+      const uint32_t lb = (uint32_t)(uintptr_t)(smem + slot * S::kSlot);
+      const uint32_t off = qa + lane < nq ? 4u * (uint32_t)lane : 0x80000000u;
+      asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
+                   :
+                   : "v"(off), "s"(lrs), "s"(4 * min(qa, nq)), "{m0}"(lb + (uint32_t)S::offLse)
+                   : "memory");
+      asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
+                   :
+                   : "v"(off), "s"(drs), "s"(4 * min(qa, nq)), "{m0}"(lb + (uint32_t)S::offD)
+                   : "memory");
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int blk = 4 * wl + j;
+      const uint32_t m0v = (uint32_t)(uintptr_t)(smem + slot * S::kSlot + (blk >= 8 ? S::offOT : S::offQT) + (blk & 7) * 1024);
+      const uint32_t vo = qa + 8 * dcm[j] < nq ? dvoff[j] : 0x80000000u;
+      // (s_nop 0: the wait state between the SALU write of M0 and the LDS-DMA that reads it)
+      asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+                   :
+                   : "v"(vo), "s"(blk >= 8 ? ors : qrs), "s"(2 * min(qa, nq)), "{m0}"(m0v)
+                   : "memory");
+    }
+  };
   auto stage = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;
+    if constexpr (DMA) {
+      // all but this wave's four (six) most recent DMAs done: tile it+1 and its row constants have landed
+      if (grp == 1) {
+        if (wl == 0) __builtin_amdgcn_s_waitcnt(0x0F76);  // vmcnt(6)
+        else __builtin_amdgcn_s_waitcnt(0x0F74);          // vmcnt(4)
+      }
+      __syncthreads();
+      if (grp == 1) dma_tile(qt0 + 32 * (it + 2), (c + 2) % 4);  // into the slot tile it-2 left
+      return;
+    }
     __syncthreads();
     store_tile((c + 1) % 4, (c + 1) % 2);         // tile it+1 (loaded in step it-2)
     load_tile(qt0 + 32 * (it + 3), (c + 1) % 2);  // tile it+3 into the set just stored
   };
   // first tiles: tile 0's loads issued now, its store after the barrier that retires the K/V images
-  load_tile(qt0, 0);
+  if constexpr (!DMA) load_tile(qt0, 0);
   auto stage0 = [&]() __attribute__((always_inline)) {
     __syncthreads();
+    if constexpr (DMA) {
+      if (grp == 1) {
+        dma_tile(qt0, 0);
+        dma_tile(qt0 + 32, 1);
+      }
+      return;
+    }
     store_tile(0, 0);
     load_tile(qt0 + 32, 1);
     load_tile(qt0 + 64, 0);
@@ -617,7 +681,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       for (int gq = 0; gq < 4; ++gq) {
         const int q4 = 16 * (gq >> 1) + 8 * h + 4 * (gq & 1);
         const floatx4 l4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 4 * q4);
-        const floatx4 d4 = *reinterpret_cast<const lds_f4_t*>(base + S::offLse + 128 + 4 * q4);
+        const floatx4 d4 = *reinterpret_cast<const lds_f4_t*>(base + S::offD + 4 * q4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           sa[4 * gq + j] = l4[j];
@@ -1643,7 +1707,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
     }
   }
   if (max(a.d, a.v_d) > 64 && v >= 0) {
-    e = v == 1404 ? launch_dkdv_pc<128, 4>(a, s) : launch_dkdv_pc<128>(a, s);
+    e = v == 1404 ? launch_dkdv_pc<128, 4>(a, s) : v == 1408 ? launch_dkdv_pc<128, 8>(a, s) : launch_dkdv_pc<128>(a, s);
     if (e != hipSuccess) return e;
     if (v == 1599 || !bwd_aligned(a)) return launch_dq<128, 4, 1, true>(a, s);
     if (v == 1604) return launch_dq_pc<128, 4>(a, s);  // stamp build (tools/dq_stamps.py)
