@@ -181,11 +181,17 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f32w_kernel(BwdArgs a) {
       pacc[i] = -base[2 * kImg + kT + 4 * g + i];
     }
     // A = Qᵀ / dOᵀ: row = query c16, k = channel 4s + g
+    // (two chains each over the even / odd k-steps: four independent MFMA chains in flight)
+    floatx4 sacc1 = {0.f, 0.f, 0.f, 0.f}, pacc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < kD / 4; ++s) {
+    for (int s = 0; s < kD / 4; s += 2) {
       sacc = mfma16(imQ[(4 * s + g) * kRP + c16], kb[s], sacc);
       pacc = mfma16(imO[(4 * s + g) * kRP + c16], vb[s], pacc);
+      sacc1 = mfma16(imQ[(4 * s + 4 + g) * kRP + c16], kb[s + 1], sacc1);
+      pacc1 = mfma16(imO[(4 * s + 4 + g) * kRP + c16], vb[s + 1], pacc1);
     }
+    sacc += sacc1;
+    pacc += pacc1;
     float p[4], ds[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -309,11 +315,16 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f32w_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { sacc[i] = negl; pacc[i] = negd; }
     // A = Kᵀ / Vᵀ: row = key c16, k = channel 4s + g
+    floatx4 sacc1 = {0.f, 0.f, 0.f, 0.f}, pacc1 = {0.f, 0.f, 0.f, 0.f};  // (four chains, as in dK/dV)
 #pragma unroll
-    for (int s = 0; s < kD / 4; ++s) {
+    for (int s = 0; s < kD / 4; s += 2) {
       sacc = mfma16(imK[(4 * s + g) * kRP + c16], qf[s], sacc);
       pacc = mfma16(imV[(4 * s + g) * kRP + c16], of[s], pacc);
+      sacc1 = mfma16(imK[(4 * s + 4 + g) * kRP + c16], qf[s + 1], sacc1);
+      pacc1 = mfma16(imV[(4 * s + 4 + g) * kRP + c16], of[s + 1], pacc1);
     }
+    sacc += sacc1;
+    pacc += pacc1;
     float ds[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
