@@ -181,14 +181,27 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f32w_kernel(BwdArgs a) {
       pacc[i] = -base[2 * kImg + kT + 4 * g + i];
     }
     // A = Qᵀ / dOᵀ: row = query c16, k = channel 4s + g
-    // (two chains each over the even / odd k-steps: four independent MFMA chains in flight)
+    // (two chains each over the even / odd k-steps: four independent MFMA chains in flight; every A
+    // operand read kAh k-steps ahead into a register rotation, so no MFMA waits on its own read)
     floatx4 sacc1 = {0.f, 0.f, 0.f, 0.f}, pacc1 = {0.f, 0.f, 0.f, 0.f};
+    constexpr int kAh = 4;
+    float aq[kAh + 1], ao[kAh + 1];
+    auto rd = [&](int n) __attribute__((always_inline)) {
+      aq[n % (kAh + 1)] = imQ[(4 * n + g) * kRP + c16];
+      ao[n % (kAh + 1)] = imO[(4 * n + g) * kRP + c16];
+    };
 #pragma unroll
-    for (int s = 0; s < kD / 4; s += 2) {
-      sacc = mfma16(imQ[(4 * s + g) * kRP + c16], kb[s], sacc);
-      pacc = mfma16(imO[(4 * s + g) * kRP + c16], vb[s], pacc);
-      sacc1 = mfma16(imQ[(4 * s + 4 + g) * kRP + c16], kb[s + 1], sacc1);
-      pacc1 = mfma16(imO[(4 * s + 4 + g) * kRP + c16], vb[s + 1], pacc1);
+    for (int n = 0; n < kAh; ++n) rd(n);
+#pragma unroll
+    for (int n = 0; n < kD / 4; ++n) {
+      if (n + kAh < kD / 4) rd(n + kAh);
+      if (n & 1) {
+        sacc1 = mfma16(aq[n % (kAh + 1)], kb[n], sacc1);
+        pacc1 = mfma16(ao[n % (kAh + 1)], vb[n], pacc1);
+      } else {
+        sacc = mfma16(aq[n % (kAh + 1)], kb[n], sacc);
+        pacc = mfma16(ao[n % (kAh + 1)], vb[n], pacc);
+      }
     }
     sacc += sacc1;
     pacc += pacc1;
@@ -207,14 +220,21 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f32w_kernel(BwdArgs a) {
       ds[i] = pv * pacc[i];
     }
     // dV += dO·P, dK += Q·dS: k-step i = queries 4g' + i; A = X[channel 16u + c16][query 4g + i]
+    // (read kAh products ahead, as above)
+    auto rdg = [&](int m) __attribute__((always_inline)) {
+      const int i = m / (kD / 16), u = m % (kD / 16), off = (16 * u + c16) * kRP + 4 * g + i;
+      ao[m % (kAh + 1)] = imO[off];
+      aq[m % (kAh + 1)] = imQ[off];
+    };
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int m = 0; m < kAh; ++m) rdg(m);
 #pragma unroll
-      for (int u = 0; u < kD / 16; ++u) {
-        const int off = (16 * u + c16) * kRP + 4 * g + i;
-        dv[u] = mfma16(imO[off], p[i], dv[u]);
-        dk[u] = mfma16(imQ[off], ds[i], dk[u]);
-      }
+    for (int m = 0; m < 4 * (kD / 16); ++m) {
+      if (m + kAh < 4 * (kD / 16)) rdg(m + kAh);
+      const int i = m / (kD / 16), u = m % (kD / 16);
+      dv[u] = mfma16(ao[m % (kAh + 1)], p[i], dv[u]);
+      dk[u] = mfma16(aq[m % (kAh + 1)], ds[i], dk[u]);
+    }
   }
 
   if (!wave_active || !key_ok) return;
@@ -315,13 +335,25 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f32w_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { sacc[i] = negl; pacc[i] = negd; }
     // A = Kᵀ / Vᵀ: row = key c16, k = channel 4s + g
-    floatx4 sacc1 = {0.f, 0.f, 0.f, 0.f}, pacc1 = {0.f, 0.f, 0.f, 0.f};  // (four chains, as in dK/dV)
+    floatx4 sacc1 = {0.f, 0.f, 0.f, 0.f}, pacc1 = {0.f, 0.f, 0.f, 0.f};  // (four chains and read-ahead, as in dK/dV)
+    constexpr int kAh = 4;
+    float ak[kAh + 1], av[kAh + 1];
+    auto rd = [&](int n) __attribute__((always_inline)) {
+      ak[n % (kAh + 1)] = imK[(4 * n + g) * kRP + c16];
+      av[n % (kAh + 1)] = imV[(4 * n + g) * kRP + c16];
+    };
 #pragma unroll
-    for (int s = 0; s < kD / 4; s += 2) {
-      sacc = mfma16(imK[(4 * s + g) * kRP + c16], qf[s], sacc);
-      pacc = mfma16(imV[(4 * s + g) * kRP + c16], of[s], pacc);
-      sacc1 = mfma16(imK[(4 * s + 4 + g) * kRP + c16], qf[s + 1], sacc1);
-      pacc1 = mfma16(imV[(4 * s + 4 + g) * kRP + c16], of[s + 1], pacc1);
+    for (int n = 0; n < kAh; ++n) rd(n);
+#pragma unroll
+    for (int n = 0; n < kD / 4; ++n) {
+      if (n + kAh < kD / 4) rd(n + kAh);
+      if (n & 1) {
+        sacc1 = mfma16(ak[n % (kAh + 1)], qf[n], sacc1);
+        pacc1 = mfma16(av[n % (kAh + 1)], of[n], pacc1);
+      } else {
+        sacc = mfma16(ak[n % (kAh + 1)], qf[n], sacc);
+        pacc = mfma16(av[n % (kAh + 1)], of[n], pacc);
+      }
     }
     sacc += sacc1;
     pacc += pacc1;
@@ -339,10 +371,17 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f32w_kernel(BwdArgs a) {
       ds[i] = pv * pacc[i];
     }
     // dQ += K·dSᵀ: k-step i = keys 4g' + i; A = K[channel 16u + c16][key 4g + i]
+    auto rdg = [&](int m) __attribute__((always_inline)) {
+      const int i = m / (kD / 16), u = m % (kD / 16);
+      ak[m % (kAh + 1)] = imK[(16 * u + c16) * kRP + 4 * g + i];
+    };
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int m = 0; m < kAh; ++m) rdg(m);
 #pragma unroll
-      for (int u = 0; u < kD / 16; ++u) dq[u] = mfma16(imK[(16 * u + c16) * kRP + 4 * g + i], ds[i], dq[u]);
+    for (int m = 0; m < 4 * (kD / 16); ++m) {
+      if (m + kAh < 4 * (kD / 16)) rdg(m + kAh);
+      dq[m % (kD / 16)] = mfma16(ak[m % (kAh + 1)], ds[m / (kD / 16)], dq[m % (kD / 16)]);
+    }
   }
 
   if (!wave_active || !q_ok) return;
