@@ -100,7 +100,9 @@ struct DkdvSmem {
 // OC > 1 (128 < d <= 256): the workgroup accumulates dK / dV for one of OC chunks of D / OC output
 // channels (chunk = block index mod OC), forming S and dP over all D channels as before: the 256-channel
 // accumulators of both gradients would not fit one wave beside the resident K' and V.
-template <int D, int NW, int WPE, int POL, bool ALN, int OC = 1>
+// RA: every LDS operand read two MFMA pairs ahead into a three-deep register rotation (diagnostic
+// variant 1420 at D = 256: measured slower there, hipcc's own placement stays).
+template <int D, int NW, int WPE, int POL, bool ALN, int OC = 1, bool RA = false>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -278,17 +280,24 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   };
   // S = Qᵀ·K', dP = dOᵀ·V: A operands (row q, k = channel) by transposed reads
   auto sdp = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) {
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      half8 qa8, oa8;
+    constexpr int kAh = RA ? 2 : 0;
+    half8 qa8[kAh + 1], oa8[kAh + 1];
+    auto rd = [&](int s) __attribute__((always_inline)) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const uint32_t off = q16_off(16 * s + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
         const half4 x = tr_read(base + S::offQT + off), y = tr_read(base + S::offOT + off);
-        if (e == 0) { qa8.lo = x; oa8.lo = y; } else { qa8.hi = x; oa8.hi = y; }
+        if (e == 0) { qa8[s % (kAh + 1)].lo = x; oa8[s % (kAh + 1)].lo = y; }
+        else { qa8[s % (kAh + 1)].hi = x; oa8[s % (kAh + 1)].hi = y; }
       }
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8, kb[s], sacc, 0, 0, 0);
-      pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8, vb[s], pacc, 0, 0, 0);
+    };
+#pragma unroll
+    for (int s = 0; s < kAh; ++s) rd(s);
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      if (s + kAh < D / 16) rd(s + kAh);
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa8[s % (kAh + 1)], kb[s], sacc, 0, 0, 0);
+      pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8[s % (kAh + 1)], vb[s], pacc, 0, 0, 0);
     }
   };
   // P = exp2(S), dS = P∘dP; k-step s of the dV / dK products = registers 8s..8s+7
@@ -323,15 +332,22 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   };
   // dV += dO·P, dK += Q·dS: A = X[row 32u + r][queries 16s + 8h + 0..7] (b128 reads of the Q16 images)
   auto dvdk = [&](const lds_char_t* base, const half8 (&pf)[2], const half8 (&sf)[2]) {
+    constexpr int kU = kDO / 32, kN = 2 * kU, kAh = RA ? 2 : 0;
+    half8 oa[kAh + 1], qa[kAh + 1];
+    auto rd = [&](int n) __attribute__((always_inline)) {  // product n = kU·s + u
+      const int s = n / kU, u = n % kU;
+      oa[n % (kAh + 1)] = read_b128(base + S::offOT + q16_off(32 * (ou0 + u) + r, 2 * s + h));
+      qa[n % (kAh + 1)] = read_b128(base + S::offQT + q16_off(32 * (ou0 + u) + r, 2 * s + h));
+    };
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int n = 0; n < kAh; ++n) rd(n);
 #pragma unroll
-      for (int u = 0; u < kDO / 32; ++u) {
-        const half8 oa = read_b128(base + S::offOT + q16_off(32 * (ou0 + u) + r, 2 * s + h));
-        const half8 qa = read_b128(base + S::offQT + q16_off(32 * (ou0 + u) + r, 2 * s + h));
-        dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa, pf[s], dv[u], 0, 0, 0);
-        dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa, sf[s], dk[u], 0, 0, 0);
-      }
+    for (int n = 0; n < kN; ++n) {
+      if (n + kAh < kN) rd(n + kAh);
+      const int s = n / kU, u = n % kU;
+      dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa[n % (kAh + 1)], pf[s], dv[u], 0, 0, 0);
+      dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[n % (kAh + 1)], sf[s], dk[u], 0, 0, 0);
+    }
   };
 
   load_tile(qt0, 0);  // unconditional, as in the dQ pass
@@ -1992,15 +2008,16 @@ hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
 
 // 128 < max(d, v_d) <= 256 (16-B aligned tensors, lengths multiples of 8): both one-wave passes at D =
 // 256, each workgroup on one of two 128-channel output chunks
+template <bool RA = false>
 hipError_t launch_bwd_wide(const BwdArgs& a, hipStream_t s) {
   constexpr int D = 256, NW = 4, OC = 2;
   const int pol = bwd_pol(a.rule);
   {
     using S = DkdvSmem<D, NW>;
     const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
-    const BwdKernel kern = pol == 0   ? bwd_dkdv_kernel<D, NW, 1, 0, true, OC>
-                           : pol == 1 ? bwd_dkdv_kernel<D, NW, 1, 1, true, OC>
-                                      : bwd_dkdv_kernel<D, NW, 1, 2, true, OC>;
+    const BwdKernel kern = pol == 0   ? bwd_dkdv_kernel<D, NW, 1, 0, true, OC, RA>
+                           : pol == 1 ? bwd_dkdv_kernel<D, NW, 1, 1, true, OC, RA>
+                                      : bwd_dkdv_kernel<D, NW, 1, 2, true, OC, RA>;
     hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb * OC)), dim3(NW * 64), S::kTotal, s, a);
@@ -2053,6 +2070,11 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(bwd_prep_kernel, dim3((unsigned)((nrows + kThrPrep - 1) / kThrPrep)), dim3(kThrPrep), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+#ifdef FA_DIAG
+  // FA_BWD_VARIANT=1420: the D = 256 dK/dV pass with its operand reads two MFMA pairs ahead (w256b
+  // backward 30.5 against 29.5 ms in one process, so not the default)
+  if (max(a.d, a.v_d) > 128 && diag_variant("FA_BWD_VARIANT") == 1420) return launch_bwd_wide<true>(a, s);
+#endif
   if (max(a.d, a.v_d) > 128) return launch_bwd_wide(a, s);
 #ifdef FA_DIAG
   // FA_BWD_VARIANT (diagnostic library): d <= 64 — 82 eight-wave blocks, 1068 / 1069 the dQ pass's

@@ -17,7 +17,7 @@ import bench  # noqa: E402
 
 def main():
     args = sys.argv[1:]
-    cfgname = args.pop(0) if args and args[0].startswith("c") else "c3"
+    cfgname = args.pop(0) if args and args[0] in bench.CONFIGS else "c3"
     variants = args or ["-1"]
     policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, _, _ = bench.CONFIGS[cfgname]
     dev = torch.device("cuda:0")
