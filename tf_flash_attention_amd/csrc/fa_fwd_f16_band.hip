@@ -90,6 +90,10 @@ constexpr int kBEpiSplit = 256;
 // conversions: at ~235 VGPRs hipcc reused two temporaries, so every v_cvt_pk_f16_f32 waited on the
 // v_exp_f32 just before it (an s_nop plus the transcendental latency, 16 times a tile)
 constexpr int kBExpBatch = 1024;
+// (staggered) the staging loads two positions ahead of their stores instead of one, in two register
+// sets (by position parity): the ablations put ≈ 0.47 ms of c4's 3.96 on the staging loads, most of it
+// their latency in front of the stores one position later
+constexpr int kBLead2 = 2048;
 constexpr int kBandR3Final = kBFPMax | kBStag | kBEpiSplit;  // round 3: staggered groups, split epilogue
 // round 4: + exponentials in batches (c4, one process: 4.109-4.147 against 4.139-4.194 ms; outputs
 // bitwise unchanged)
@@ -317,7 +321,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   // ---- prologue: Q(item 0) into Q buffer 0, K(0..2) into ring slots 0..2, V(0..1) into slots
   //      0..1 (slot 3 zeroed: the first PV reads "V(-1)" against P = 0), K(3..4) / V(2..3) into
   //      the staging registers (positions 0..5 all belong to item 0: T >= 6)
+  constexpr bool LEAD2 = STG && (F & kBLead2) != 0;
   u32x4 kst[2], vst[2];
+  u32x4 kst2[LEAD2 ? 2 : 1][2], vst2[LEAD2 ? 2 : 1][2];  // LEAD2: set p & 1 feeds the stores at position p
   {
     u32x4 kp[3], vp[2], qv[4];
 #pragma unroll
@@ -326,7 +332,12 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     for (int j = 0; j < 2; ++j) vp[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + j * kBN);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      if constexpr (STG) {  // the chunks this thread's group stores at position 0
+      if constexpr (LEAD2) {  // the chunks this thread's group stores at positions 0 and 1
+        kst2[0][j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 0, 1, j) : stag_k1(T, 0, 0, j)) * kBN);
+        vst2[0][j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 0, 1, j) : stag_v1(T, 0, 0, j)) * kBN);
+        kst2[1][j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 1, 1, j) : stag_k1(T, 1, 0, j)) * kBN);
+        vst2[1][j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 1, 1, j) : stag_v1(T, 1, 0, j)) * kBN);
+      } else if constexpr (STG) {  // the chunks this thread's group stores at position 0
         kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 0, 1, j) : stag_k1(T, 0, 0, j)) * kBN);
         vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 0, 1, j) : stag_v1(T, 0, 0, j)) * kBN);
       } else {
@@ -771,12 +782,12 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         static_for<0, stag_nk(T, it)>([&](auto I_) __attribute__((always_inline)) {
           constexpr int i = decltype(I_)::value, j0 = stag_k1(T, it, 0, i), j1 = stag_k1(T, it, 1, i);
           const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
-          store(kOffK + (j & 3) * kTile + kwo, kst[i]);
+          store(kOffK + (j & 3) * kTile + kwo, LEAD2 ? kst2[(it & 1) % (LEAD2 ? 2 : 1)][i] : kst[i]);
         });
         static_for<0, stag_nv(T, it)>([&](auto I_) __attribute__((always_inline)) {
           constexpr int i = decltype(I_)::value, j0 = stag_v1(T, it, 0, i), j1 = stag_v1(T, it, 1, i);
           const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
-          store(kOffV + (j & 3) * kTile + vwo, vst[i]);
+          store(kOffV + (j & 3) * kTile + vwo, LEAD2 ? vst2[(it & 1) % (LEAD2 ? 2 : 1)][i] : vst[i]);
         });
       }
     } else if constexpr (!(F & kBANoStore)) {
@@ -821,7 +832,31 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       }
     }
     if constexpr (it >= 2 && it <= 5) qst = qload(nxt, it - 2);
-    if constexpr (STG) {
+    if constexpr (STG && (F & kBANoLoad) != 0) {
+      // timing ablation (outputs WRONG): no staging loads, the stores write stale registers
+    } else if constexpr (LEAD2) {
+      // the chunks the group stores two positions on (the next item's positions 0 / 1 at T-2 / T-1),
+      // into the set those stores read; tile j of the current item, or j - NT of the next
+      constexpr int pn = it + 2 < T ? it + 2 : it + 2 - T, add = it + 2 < T ? 0 : NT, set = (it & 1) % (LEAD2 ? 2 : 1);
+      auto src = [&](int j0, int j1, uint32_t slsz, int& slb, int& k0) __attribute__((always_inline)) {
+        const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
+        const bool nx = j >= NT;
+        slb = (nx ? nxt.sl : cur.sl) * (int)slsz;
+        k0 = (nx ? nxt.kt0 : cur.kt0) + (nx ? j - NT : j) * kBN;
+      };
+      static_for<0, stag_nk(T, pn)>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = decltype(I_)::value;
+        int slb, k0;
+        src(stag_k1(T, pn, 0, i) + add, stag_k1(T, pn, 1, i) + add, ksl, slb, k0);
+        kst2[set][i] = load(krs, koff, (uint32_t)slb, k0);
+      });
+      static_for<0, stag_nv(T, pn)>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = decltype(I_)::value;
+        int slb, k0;
+        src(stag_v1(T, pn, 0, i) + add, stag_v1(T, pn, 1, i) + add, vsl, slb, k0);
+        vst2[set][i] = load(vrs, voff, (uint32_t)slb, k0);
+      });
+    } else if constexpr (STG) {
       // the chunks the group stores at the next position (the next item's position 0 at T-1), one
       // position ahead; tile j of the current item, or j - NT of the next
       constexpr int pn = it + 1 < T ? it + 1 : 0, add = it + 1 < T ? 0 : NT;
@@ -1081,6 +1116,12 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   if (dv == 2421 && ba.T == 10) return launch_band_t<10, true>(ba, s);
   if (dv == 2422 && ba.T == 10) return launch_band_t<10, false, kBFPMax | kBStag | kBExpBatch>(ba, s);  // epilogue in VALU(0)
   if (dv == 2424 && ba.T == 10) return launch_band_t<10, false, kBandR3Final>(ba, s);  // round-3 default
+  // timing ablations of the default (outputs WRONG): no edge masks, no softmax, no staging stores
+  if (dv == 2425 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoMask>(ba, s);
+  if (dv == 2426 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoSoftmax>(ba, s);
+  if (dv == 2427 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoStore>(ba, s);
+  if (dv == 2428 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoLoad>(ba, s);
+  if (dv == 2429 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBLead2>(ba, s);
 #endif
   switch (ba.T) {
     case 10: return launch_band_t<10>(ba, s);
