@@ -91,9 +91,16 @@ constexpr int kBEpiSplit = 256;
 // v_exp_f32 just before it (an s_nop plus the transcendental latency, 16 times a tile)
 constexpr int kBExpBatch = 1024;
 // (staggered) the staging loads two positions ahead of their stores instead of one, in two register
-// sets (by position parity): the ablations put ≈ 0.47 ms of c4's 3.96 on the staging loads, most of it
-// their latency in front of the stores one position later
+// sets (by position parity).  Measured within 0.5 % of one position: not taken
 constexpr int kBLead2 = 2048;
+// (staggered) the staging by LDS-DMA (inline-asm `buffer_load_dwordx4 ... lds`, no staging registers,
+// no ds_write_b128): each wave fetches its 8 channel rows of a group's tile chunk straight into the
+// ring slot at the point the register form stored it, the lanes' source chunks permuted so the
+// contiguous 1 KB the wave writes is the swizzled row image; every wave waits vmcnt(0) at the end of
+// the next VALU phase, before the barrier that publishes the slot (hipcc does not see these loads)
+constexpr int kBDma = 4096;
+// timing ablation of kBDma (outputs WRONG): no vmcnt wait before the publishing barrier
+constexpr int kBANoDmaWait = 8192;
 constexpr int kBandR3Final = kBFPMax | kBStag | kBEpiSplit;  // round 3: staggered groups, split epilogue
 // round 4: + exponentials in batches (c4, one process: 4.109-4.147 against 4.139-4.194 ms; outputs
 // bitwise unchanged)
@@ -298,6 +305,20 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     return __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off : 0x80000000u, slb + 2 * min(k0, nk), 0);
   };
   auto store = [&](int off, u32x4 v) __attribute__((always_inline)) { *reinterpret_cast<lds_u32x4_t*>(smem + off) = v; };
+  // (kBDma) lane L of wave w writes LDS bytes 1024 w + 16 L of the slot: channel row crow = tid >> 3,
+  // in-row chunk tid & 7, so it fetches the global chunk the swizzle puts there (kwo / vwo inverted)
+  auto dma = [&](__amdgpu_buffer_rsrc_t rs, bool isk, uint32_t slb, int k0, int lds_off) __attribute__((always_inline)) {
+    int t = tid;
+    asm volatile("" : "+v"(t));  // (recomputed where used: hoisted, the offsets would stay live)
+    const int rw = t >> 3;
+    const int cmx = isk ? ((t & 7) ^ ((rw & 2) << 1)) : ((t & 7) ^ ((rw >> 1) & 7));
+    const bool in = rw < (isk ? d : vd) && k0 >= 0 && k0 + 8 * cmx < nk;
+    const uint32_t off = in ? (uint32_t)rw * (uint32_t)nk * 2u + 16u * cmx : 0x80000000u;
+    const uint32_t m0v = (uint32_t)(uintptr_t)(smem + lds_off) + 1024u * (uint32_t)w;
+    const uint32_t so = __builtin_amdgcn_readfirstlane(slb + 2 * min(max(k0, 0), nk));
+    // (s_nop 0: the one wait state between the SALU write of M0 and an LDS-DMA that reads it)
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(off), "s"(rs), "s"(so), "{m0}"(m0v) : "memory");
+  };
   //      Q image [64][256] (64-B blocks XOR-swizzled by c&3): chunk j of a thread = channel row
   //      (tid>>5) + 16j, 8 queries at 8*(tid&31)
   const int qc0 = tid >> 5, qm = tid & 31;
@@ -337,6 +358,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         vst2[0][j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 0, 1, j) : stag_v1(T, 0, 0, j)) * kBN);
         kst2[1][j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 1, 1, j) : stag_k1(T, 1, 0, j)) * kBN);
         vst2[1][j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 1, 1, j) : stag_v1(T, 1, 0, j)) * kBN);
+      } else if constexpr (STG && (F & kBDma) != 0) {  // (position 0's chunks fetched in MFMA(0))
       } else if constexpr (STG) {  // the chunks this thread's group stores at position 0
         kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 0, 1, j) : stag_k1(T, 0, 0, j)) * kBN);
         vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 0, 1, j) : stag_v1(T, 0, 0, j)) * kBN);
@@ -778,7 +800,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // PV k-steps 2-3
     // staging: K(+3), V(+2) into the ring; loads of K(+5), V(+4) (this item's or the next's)
     if constexpr (STG) {  // the group's tiles of this position (stag_k1 / stag_v1), tile j in slot j & 3
-      if constexpr (!(F & kBANoStore)) {
+      if constexpr (!(F & kBANoStore) && !(F & kBDma)) {
         static_for<0, stag_nk(T, it)>([&](auto I_) __attribute__((always_inline)) {
           constexpr int i = decltype(I_)::value, j0 = stag_k1(T, it, 0, i), j1 = stag_k1(T, it, 1, i);
           const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
@@ -834,6 +856,27 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     if constexpr (it >= 2 && it <= 5) qst = qload(nxt, it - 2);
     if constexpr (STG && (F & kBANoLoad) != 0) {
       // timing ablation (outputs WRONG): no staging loads, the stores write stale registers
+    } else if constexpr (STG && (F & kBDma) != 0) {
+      // this position's chunks straight into their ring slots (where the register form stores them;
+      // the slots' previous tiles are dead here); tile j of the current item, or j - NT of the next
+      auto src = [&](int j0, int j1, uint32_t slsz, int& slb, int& k0) __attribute__((always_inline)) {
+        const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
+        const bool nx = j >= NT;
+        slb = (nx ? nxt.sl : cur.sl) * (int)slsz;
+        k0 = (nx ? nxt.kt0 : cur.kt0) + (nx ? j - NT : j) * kBN;
+      };
+      static_for<0, stag_nk(T, it)>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = decltype(I_)::value, j0 = stag_k1(T, it, 0, i), j1 = stag_k1(T, it, 1, i);
+        int slb, k0;
+        src(j0, j1, ksl, slb, k0);
+        dma(krs, true, (uint32_t)slb, k0, kOffK + ((((j0 == j1) ? j0 : (grp ? j1 : j0))) & 3) * kTile);
+      });
+      static_for<0, stag_nv(T, it)>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = decltype(I_)::value, j0 = stag_v1(T, it, 0, i), j1 = stag_v1(T, it, 1, i);
+        int slb, k0;
+        src(j0, j1, vsl, slb, k0);
+        dma(vrs, false, (uint32_t)slb, k0, kOffV + ((((j0 == j1) ? j0 : (grp ? j1 : j0))) & 3) * kTile);
+      });
     } else if constexpr (LEAD2) {
       // the chunks the group stores two positions on (the next item's positions 0 / 1 at T-2 / T-1),
       // into the set those stores read; tile j of the current item, or j - NT of the next
@@ -944,6 +987,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
 #pragma unroll
       for (int i = 0; i < 16; ++i) negm[i] = 0.f;
     }
+    // (kBDma) this wave's chunks fetched in the MFMA phase before have landed: the barrier after this
+    // phase publishes them, two intervals after their issue, as the register form's stores
+    if constexpr (STG && (F & kBDma) != 0 && (F & kBANoDmaWait) == 0) __builtin_amdgcn_s_waitcnt(0x0F70);
   };
 
   if (grp == 1) __builtin_amdgcn_s_barrier();
@@ -1122,6 +1168,8 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   if (dv == 2427 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoStore>(ba, s);
   if (dv == 2428 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoLoad>(ba, s);
   if (dv == 2429 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBLead2>(ba, s);
+  if (dv == 2430 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBDma>(ba, s);
+  if (dv == 2431 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBDma | kBANoDmaWait>(ba, s);
 #endif
   switch (ba.T) {
     case 10: return launch_band_t<10>(ba, s);
