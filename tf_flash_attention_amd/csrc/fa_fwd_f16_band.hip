@@ -101,6 +101,10 @@ constexpr int kBLead2 = 2048;
 constexpr int kBDma = 4096;
 // timing ablation of kBDma (outputs WRONG): no vmcnt wait before the publishing barrier
 constexpr int kBANoDmaWait = 8192;
+// the edge mask's bounds as fp32 pairs (v_pk_add_f32: each pair the previous plus 2 or 10 key steps,
+// exact: multiples of 2^99 below 2^113), 16 packed adds instead of 32 v_fmamk; bitwise unchanged,
+// 2-3 % slower on c4 (one dependent chain): diagnostic only
+constexpr int kBMaskPk = 16384;
 constexpr int kBandR3Final = kBFPMax | kBStag | kBEpiSplit;  // round 3: staggered groups, split epilogue
 // round 4: + exponentials in batches (c4, one process: 4.109-4.147 against 4.139-4.194 ms; outputs
 // bitwise unchanged)
@@ -506,6 +510,20 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     for (int pass = 0; pass < npass; ++pass) {
       const bool lo = (cls == 3) || (cls == 1 && pass == 0);
       const float cc = lo ? ca : cb, sg = lo ? kBig : -kBig;
+      if constexpr ((F & kBMaskPk) != 0) {
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        f2v bnd = {cc, cc + sg};  // keys 0, 1 of the tile (relative to the lane's half)
+        const f2v d2 = {2.f * sg, 2.f * sg}, d10 = {10.f * sg, 10.f * sg};
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) {
+            if (t + i > 0) bnd += (i & 7) == 0 ? d10 : d2;  // key 32t + 16(i>>3) + (i&7)
+            st[t][i] = fminf(st[t][i], bnd.x);
+            st[t][i + 1] = fminf(st[t][i + 1], bnd.y);
+          }
+        continue;
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1170,6 +1188,7 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   if (dv == 2429 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBLead2>(ba, s);
   if (dv == 2430 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBDma>(ba, s);
   if (dv == 2431 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBDma | kBANoDmaWait>(ba, s);
+  if (dv == 2432 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBMaskPk>(ba, s);
 #endif
   switch (ba.T) {
     case 10: return launch_band_t<10>(ba, s);
