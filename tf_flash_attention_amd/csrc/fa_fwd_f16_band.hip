@@ -105,6 +105,8 @@ constexpr int kBANoDmaWait = 8192;
 // exact: multiples of 2^99 below 2^113), 16 packed adds instead of 32 v_fmamk; bitwise unchanged,
 // 2-3 % slower on c4 (one dependent chain): diagnostic only
 constexpr int kBMaskPk = 16384;
+// (with kBMaskPk) the pairs as two independent chains of eight, one per 32-key half
+constexpr int kBMaskPk2 = 32768;
 constexpr int kBandR3Final = kBFPMax | kBStag | kBEpiSplit;  // round 3: staggered groups, split epilogue
 // round 4: + exponentials in batches (c4, one process: 4.109-4.147 against 4.139-4.194 ms; outputs
 // bitwise unchanged)
@@ -512,8 +514,20 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       const float cc = lo ? ca : cb, sg = lo ? kBig : -kBig;
       if constexpr ((F & kBMaskPk) != 0) {
         typedef float f2v __attribute__((ext_vector_type(2)));
-        f2v bnd = {cc, cc + sg};  // keys 0, 1 of the tile (relative to the lane's half)
         const f2v d2 = {2.f * sg, 2.f * sg}, d10 = {10.f * sg, 10.f * sg};
+        if constexpr ((F & kBMaskPk2) != 0) {  // two independent chains (t = 0, 1), interleaved
+          f2v b[2] = {{cc, cc + sg}, {cc + 32.f * sg, cc + 33.f * sg}};
+#pragma unroll
+          for (int i = 0; i < 16; i += 2)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              if (i > 0) b[t] += (i & 7) == 0 ? d10 : d2;
+              st[t][i] = fminf(st[t][i], b[t].x);
+              st[t][i + 1] = fminf(st[t][i + 1], b[t].y);
+            }
+          continue;
+        }
+        f2v bnd = {cc, cc + sg};  // keys 0, 1 of the tile (relative to the lane's half)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1189,6 +1203,7 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   if (dv == 2430 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBDma>(ba, s);
   if (dv == 2431 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBDma | kBANoDmaWait>(ba, s);
   if (dv == 2432 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBMaskPk>(ba, s);
+  if (dv == 2433 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBMaskPk | kBMaskPk2>(ba, s);
 #endif
   switch (ba.T) {
     case 10: return launch_band_t<10>(ba, s);
