@@ -295,3 +295,34 @@ def test_cpu_tensors_fail_loudly():
     x = torch.zeros(1, 2, 8, 16)
     with pytest.raises(fa.InvalidArgumentError, match="no CPU kernel"):
         fa.full_1d(x, x, x)
+
+
+def test_using_override_rejects_overlap_across_threads():
+    """_lib.using() routes the whole process; a second thread may not open a block while
+    another thread's block is open (nesting within one thread is fine)."""
+    import threading
+    path = _lib.LIB_PATH
+    errors = []
+    inside = threading.Event()
+    release = threading.Event()
+
+    def holder():
+        with _lib.using(path):
+            with _lib.using(path):  # nested, same thread
+                inside.set()
+                release.wait(10)
+
+    t = threading.Thread(target=holder)
+    t.start()
+    assert inside.wait(10)
+    try:
+        with _lib.using(path):
+            pass
+    except RuntimeError as e:
+        errors.append(str(e))
+    finally:
+        release.set()
+        t.join(10)
+    assert errors and "another thread" in errors[0]
+    with _lib.using(path):  # free again once the holder's blocks have closed
+        pass

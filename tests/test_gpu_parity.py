@@ -198,6 +198,46 @@ def test_reference_matrix(dtype, seq_dims, case):
     run_case(dtype, policy, seq_dims, mode, (1, 3), d, d, qs, ks, ws, ls, causal, seed=1)
 
 
+# The same 16-case matrix at the reference's own shape ranges (tests/test_1d.py:57-66,
+# tests/test_2d.py:85-94): [B, H, C, *seq] from [1, 8, 8, 256] to [1, 8, 32, N_max] in 1d with
+# N_max = 4096 / 2048 / 1024 for fp16 / fp32 / fp64, and from [1, 8, 8, 16, 16] to
+# [1, 8, 32, 64, 64] / [.., 32, 64] / [.., 32, 32] in 2d.  Two draws per case, as the reference's
+# test_base.py:148-176 makes them: 'max' (Q = K = V = the max shape) and 'random' (C and the K
+# sequence drawn in range, the Q sequence drawn separately, so Nq != Nk; fp16 rounds the last
+# sequence dim to even).  The oracle checks the first and last of the 8 slices.
+REF_SHAPES = {
+    1: {np.float16: (256, 4096), np.float32: (256, 2048), np.float64: (256, 1024)},
+    2: {np.float16: ((16, 16), (64, 64)), np.float32: ((16, 16), (32, 64)), np.float64: ((16, 16), (32, 32))},
+}
+
+
+def _ref_draw(dtype, seq_dims, case, draw):
+    if draw == "max":
+        mx = REF_SHAPES[seq_dims][dtype][1]
+        qs = ks = (mx,) if seq_dims == 1 else tuple(mx)
+        return 32, qs, ks
+    rng = np.random.default_rng(zlib.crc32(repr((np.dtype(dtype).name, seq_dims) + case).encode()))
+    lo, hi = REF_SHAPES[seq_dims][dtype]
+    lo, hi = ((lo,), (hi,)) if seq_dims == 1 else (lo, hi)
+    d = int(rng.integers(8, 33))
+    ks = tuple(int(rng.integers(a, b + 1)) for a, b in zip(lo, hi))
+    qs = tuple(int(rng.integers(a, b + 1)) for a, b in zip(lo, hi))
+    if dtype == np.float16:
+        ks, qs = ks[:-1] + (ks[-1] // 2 * 2,), qs[:-1] + (qs[-1] // 2 * 2,)
+    return d, qs, ks
+
+
+@pytest.mark.parametrize("draw", ["max", "random"])
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
+@pytest.mark.parametrize("seq_dims", [1, 2])
+@pytest.mark.parametrize("case", REF_CASES, ids=lambda c: f"{c[0]}-{c[1]}-s{int(c[2])}-c{int(c[3])}")
+def test_reference_matrix_reference_shapes(draw, dtype, seq_dims, case):
+    policy, mode, stride, causal = case
+    d, qs, ks = _ref_draw(dtype, seq_dims, case, draw)
+    ws, ls = _ref_window(seq_dims, qs, ks, stride)
+    run_case(dtype, policy, seq_dims, mode, (1, 8), d, d, qs, ks, ws, ls, causal, seed=2, slices=[0, 7])
+
+
 # ------------------------------------------------- small windows / strides
 @pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
 @pytest.mark.parametrize("seq_dims,qs,ks", [(1, (300,), (300,)), (1, (257,), (130,)), (1, (130,), (517,)),
@@ -345,6 +385,9 @@ def test_wide_channels(dtype, d, vd, policy, ws, causal):
 @pytest.mark.parametrize("d,vd", [(256, 256), (160, 160), (130, 200), (200, 64), (64, 256)])
 @pytest.mark.parametrize("policy,mode,qs,ks,ws,causal", [
     ("full", "none_front", (300,), (520,), 1, False),
+    # square causal, nk % 8 == 0 with a ragged query block: the wide MFMA kernel itself (heaviest
+    # blocks first, diagonal edge tiles on every block); 777 (nk % 8 != 0) runs the SIMT fallback
+    ("causal", "none_front", (776,), (776,), 1, False),
     ("causal", "none_front", (777,), (777,), 1, False),
     ("causal", "scale_end", (200,), (520,), 1, False),
     ("local", "scale_front", (240,), (480,), 70, True),

@@ -69,6 +69,8 @@ _tls = threading.local()  # .override: a library routed in by using() on THIS th
 # its own device thread, which does not see the thread-local override of the thread that called
 # .backward() (the diag-variant backward tests otherwise ran the product library)
 _process_override = None
+_process_owner = None   # thread ident of the using() block that set _process_override
+_process_depth = 0
 _loaded = {}
 DIAG_LIB_PATH = os.path.join(_HERE, "libfa_hip_diag.so")
 
@@ -136,23 +138,33 @@ def using(path):
     the product library.  ctypes loads each library RTLD_LOCAL, so both can live in one process.
     The routing covers this thread and, while the block runs, every other thread of the process
     (autograd's device thread runs the backward of a CUDA tensor); blocks do not nest across
-    threads."""
-    global _process_override
+    threads: a second thread entering ``using()`` while another thread's block is open raises."""
+    global _process_override, _process_owner, _process_depth
+    me = threading.get_ident()
     with _lock:
+        if _process_owner is not None and _process_owner != me:
+            raise RuntimeError("_lib.using(): another thread's library override is active; "
+                               "blocks may not overlap across threads")
         h = _loaded.get(path)
         if h is None:
             if not os.path.exists(path):
                 raise LibraryNotBuiltError(f"library not found at {path}")
             h = _loaded[path] = _declare(ctypes.CDLL(path))
-    prev = getattr(_tls, "override", None)
-    prev_proc = _process_override
-    _tls.override = h
-    _process_override = h
+        prev = getattr(_tls, "override", None)
+        prev_proc = _process_override
+        _tls.override = h
+        _process_override = h
+        _process_owner = me
+        _process_depth += 1
     try:
         yield h
     finally:
-        _tls.override = prev
-        _process_override = prev_proc
+        with _lock:
+            _tls.override = prev
+            _process_override = prev_proc
+            _process_depth -= 1
+            if _process_depth == 0:
+                _process_owner = None
 
 
 def make_problem(dtype, policy, seq_dims, sync_mode, b, q_seq, k_seq, d, v_d,

@@ -359,13 +359,16 @@ bool bwd_f16_supported(const BwdArgs& a) {
 
 hipError_t launch_bwd_f16(const BwdArgs& a, hipStream_t s) {
   // the two-pass kernels take the shapes they support (diagnostic library: FA_BWD_VARIANT=0 pins
-  // this single-pass atomic kernel for A/B runs)
+  // this single-pass atomic kernel for A/B runs; it holds at most 128 channels, so shapes past
+  // that always go to the two-pass kernels)
+  const int dm = max(a.d, a.v_d);
 #ifdef FA_DIAG
-  const bool pinned = diag_variant("FA_BWD_VARIANT") == 0;
+  const bool pinned = diag_variant("FA_BWD_VARIANT") == 0 && dm <= 128;
 #else
   constexpr bool pinned = false;
 #endif
   if (!pinned && bwd_f16_fast_supported(a)) return launch_bwd_f16_fast(a, s);
+  if (dm > 128) return hipErrorInvalidValue;
   const int nq = a.rule.q.n;
   hipError_t e = hipMemsetAsync(a.ws_dQ, 0, sizeof(float) * (size_t)a.b * a.d * nq, s);
   if (e != hipSuccess) return e;
@@ -374,7 +377,6 @@ hipError_t launch_bwd_f16(const BwdArgs& a, hipStream_t s) {
                      a);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int dm = max(a.d, a.v_d);
   e = dm <= 32 ? launch_main<32>(a, s) : (dm <= 64 ? launch_main<64>(a, s) : launch_main<128>(a, s));
   if (e != hipSuccess) return e;
   const int64_t n = a.b * (int64_t)a.d * nq;
