@@ -576,13 +576,9 @@ def test_f16_forward_structures_d128(monkeypatch, diag_lib, variant, policy, seq
 
 
 # backward structures kept in the diagnostic library: 1599 = the one-wave dQ pass (the structure the
-# unaligned d > 64 shapes ship with) on aligned shapes, 1404 / 1604 = the producer / consumer dK/dV and
-# dQ passes' stamp builds (stamps go to the unused dQ workspace: gradients unchanged), 1068 / 1069 = the d <= 64
-# dQ pass with run-ahead operand reads, 1071 = its edge mask as a branch, 82 = the d <= 64 passes in
-# eight-wave blocks, 1408 = the d = 128 dK/dV pass staged by the consumers' LDS-DMA, 1416 = the four-role
-# dK/dV pass
-@pytest.mark.parametrize("variant,d", [("1599", 128), ("1404", 128), ("1604", 128), ("1068", 64), ("1069", 48), ("1071", 64),
-                                       ("82", 64), ("1408", 128), ("1416", 128)])
+# unaligned d > 64 shapes ship with) on aligned shapes, 1068 / 1069 = the d <= 64 dQ pass with run-ahead
+# operand reads, 1071 = its edge mask as a branch, 82 = the d <= 64 passes in eight-wave blocks
+@pytest.mark.parametrize("variant,d", [("1599", 128), ("1068", 64), ("1069", 48), ("1071", 64), ("82", 64)])
 @pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, True)])
 def test_f16_backward_read_placement(monkeypatch, diag_lib, variant, d, policy, ws, causal):
     monkeypatch.setenv("FA_BWD_VARIANT", variant)

@@ -437,7 +437,7 @@ struct PcSmem {
   static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;  // the K/V images alias the ring
 };
 
-template <int D, int POL, bool ALN, int PF = 0>
+template <int D, int POL, bool ALN>
 __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -447,26 +447,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   constexpr int kQChunks = D * 4;                 // 16-B chunks of one [D][32] tile
   static_assert((2 * kQChunks) % kThr == 0, "tile chunks must divide over the workgroup");
   constexpr int kCPT = 2 * kQChunks / kThr;       // Q and dO chunks per thread
-  // PF & 4 (diagnostic build): per-wave s_memtime sums of each step's parts (stage + barrier, MFMA
-  // part, softmax / hand-over part) written to the unused dQ workspace
-  constexpr bool STAMP = (PF & 4) != 0;
-  // PF & 8: the query tiles staged by the consumer waves alone, as LDS-DMA issued by inline assembly
-  // (tile it+2 into the free ring slot at step it; hand-counted vmcnt before each barrier), so the
-  // producers, the step's critical path, carry no staging at all (16-B aligned shapes, D = 128)
-  constexpr bool DMA = (PF & 8) != 0 && ALN;
-  static_assert(!DMA || D == 128, "the LDS-DMA staging assumes 16 1-KB blocks a tile, four a consumer wave");
-  uint64_t stv[3] = {0, 0, 0}, st_prev = 0;
-  auto stamp = [&](int k) __attribute__((always_inline)) {
-    if constexpr (STAMP) {
-      __builtin_amdgcn_sched_barrier(0);
-      uint64_t t;
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      if (k >= 0) stv[k] += t - st_prev;
-      st_prev = t;
-    }
-  };
-
   const int nq = a.rule.q.n, nk = a.rule.k.n;
   const uint32_t nkb = (nk + kBK - 1) / kBK;
   const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -474,15 +454,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   const int k0 = (int)(bid % nkb) * kBK;  // earliest (heaviest under causal) key blocks first
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = w >> 2, wl = w & 3;
-  auto stamp_out = [&]() __attribute__((always_inline)) {
-    if constexpr (STAMP) {
-      if (lane < 3) {
-        uint64_t v = lane == 0 ? stv[0] : lane == 1 ? stv[1] : stv[2];
-        reinterpret_cast<uint64_t*>(a.ws_dQ)[((int64_t)bid * 8 + w) * 4 + lane] = v;
-      }
-    }
-  };     // group 0 produces, group 1 consumes; wl: the key slice
+  const int grp = w >> 2, wl = w & 3;  // group 0 produces, group 1 consumes; wl: the key slice
   const int h = lane >> 5, r = lane & 31;
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const int sig = ((tp & 1) << 1) | (tp >> 1);  // (see the dK/dV kernel above: σ-permuted transposed reads)
@@ -599,75 +571,16 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
   // compile-time); loads and stores are unconditional (phantom tiles move zeros), so hipcc's vmcnt
   // waits stay exact.
   const int nsteps = ntiles + 1;
-  // ---- DMA staging (PF & 8): consumer wave wl issues the 1-KB blocks 4wl .. 4wl+3 of a tile (0-7 the
-  // Q16 image, 8-15 the dO16 image; block b = channel rows 16b .. 16b+15, lane L the 16 B at 16L =
-  // row 16b + L/4, position L%4, i.e. source chunk (L%4) ^ swizzle(row)); wave 4 also moves the row
-  // constants, -lse2 and -D of queries qa .. qa+63 by two dword LDS-DMAs (the first 32 used).  Past
-  // nq they read 0, not -inf / 0: those queries' Q and dO are zero too, so S = dP = D = 0, P = 1 and
-  // their dV / dK terms (dO·P, Q·dS with dS = P·(dP - D)) vanish all the same.
-  uint32_t dvoff[4];
-  int dcm[4];
-  const __amdgpu_buffer_rsrc_t lrs = make_rsrc(glse, 4u * nq), drs = make_rsrc(gD, 4u * nq);
-  if constexpr (DMA) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int blk = 4 * wl + j, b = blk & 7, row = 16 * b + (lane >> 2);
-      dcm[j] = (lane & 3) ^ ((row >> 2) & 3);
-      dvoff[j] = row < (blk >= 8 ? vd : d) ? (uint32_t)row * (uint32_t)nq * 2u + 16u * dcm[j] : 0x80000000u;
-    }
-  }
-  auto dma_tile = [&](int qa, int slot) __attribute__((always_inline)) {
-    if (wl == 0) {
-      const uint32_t lb = (uint32_t)(uintptr_t)(smem + slot * S::kSlot);
-      const uint32_t off = qa + lane < nq ? 4u * (uint32_t)lane : 0x80000000u;
-      asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
-                   :
-                   : "v"(off), "s"(lrs), "s"(4 * min(qa, nq)), "{m0}"(lb + (uint32_t)S::offLse)
-                   : "memory");
-      asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
-                   :
-                   : "v"(off), "s"(drs), "s"(4 * min(qa, nq)), "{m0}"(lb + (uint32_t)S::offD)
-                   : "memory");
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int blk = 4 * wl + j;
-      const uint32_t m0v = (uint32_t)(uintptr_t)(smem + slot * S::kSlot + (blk >= 8 ? S::offOT : S::offQT) + (blk & 7) * 1024);
-      const uint32_t vo = qa + 8 * dcm[j] < nq ? dvoff[j] : 0x80000000u;
-      // (s_nop 0: the wait state between the SALU write of M0 and the LDS-DMA that reads it)
-      asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
-                   :
-                   : "v"(vo), "s"(blk >= 8 ? ors : qrs), "s"(2 * min(qa, nq)), "{m0}"(m0v)
-                   : "memory");
-    }
-  };
   auto stage = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;
-    if constexpr (DMA) {
-      // all but this wave's four (six) most recent DMAs done: tile it+1 and its row constants have landed
-      if (grp == 1) {
-        if (wl == 0) __builtin_amdgcn_s_waitcnt(0x0F76);  // vmcnt(6)
-        else __builtin_amdgcn_s_waitcnt(0x0F74);          // vmcnt(4)
-      }
-      __syncthreads();
-      if (grp == 1) dma_tile(qt0 + 32 * (it + 2), (c + 2) % 4);  // into the slot tile it-2 left
-      return;
-    }
     __syncthreads();
     store_tile((c + 1) % 4, (c + 1) % 2);         // tile it+1 (loaded in step it-2)
     load_tile(qt0 + 32 * (it + 3), (c + 1) % 2);  // tile it+3 into the set just stored
   };
   // first tiles: tile 0's loads issued now, its store after the barrier that retires the K/V images
-  if constexpr (!DMA) load_tile(qt0, 0);
+  load_tile(qt0, 0);
   auto stage0 = [&]() __attribute__((always_inline)) {
     __syncthreads();
-    if constexpr (DMA) {
-      if (grp == 1) {
-        dma_tile(qt0, 0);
-        dma_tile(qt0 + 32, 1);
-      }
-      return;
-    }
     store_tile(0, 0);
     load_tile(qt0 + 32, 1);
     load_tile(qt0 + 64, 0);
@@ -716,9 +629,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
     };
     auto pstep = [&](auto C_, int it) __attribute__((always_inline)) {
       constexpr int c = decltype(C_)::value;
-      stamp(-1);
       stage(C_, it);
-      stamp(0);
       const int qa = qt0 + 32 * it;
       const int cls = it < ntiles ? tcls(qa) : 0;
       const lds_char_t* base = smem + c * S::kSlot;
@@ -740,7 +651,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
           pacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa8[s_ % (kAh + 1)], vb[s_], pacc, 0, 0, 0);
         }
       }
-      stamp(1);
       if (cls == 0) return;
       // P = exp2(S), dS = P∘dP; register i = query 16(i>>3) + 8h + (i&7) = k-step i>>3 of the consumer
       half8 pf[2], sf[2];
@@ -774,7 +684,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
         *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, s_)) = pf[s_];
         *reinterpret_cast<lds_half8_t*>(smem + xoff(c % 2, 2 + s_)) = sf[s_];
       }
-      stamp(2);
     };
     for (int it = 0; it < nsteps; it += 4) {
       pstep(IC<0>{}, it);
@@ -782,7 +691,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       pstep(IC<2>{}, it + 2);
       pstep(IC<3>{}, it + 3);
     }
-    stamp_out();
     return;
   }
 
@@ -795,9 +703,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
     for (int i = 0; i < 16; ++i) { dk[u][i] = 0.f; dv[u][i] = 0.f; }
   auto cstep = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;
-    stamp(-1);
     stage(C_, it);
-    stamp(0);
     const int qa = qt0 + 32 * (it - 1);
     const int cls = (it >= 1 && it - 1 < ntiles) ? tcls(qa) : 0;
     const lds_char_t* base = smem + ((c + 3) % 4) * S::kSlot;
@@ -818,7 +724,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
 #pragma unroll
       for (int n = 0; n < kAh; ++n) rd(n);
     }
-    stamp(1);
     if (cls == 0) return;
 #pragma unroll
     for (int n = 0; n < kN; ++n) {
@@ -827,7 +732,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       dv[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(oa[n % (kAh + 1)], pf[s_], dv[u], 0, 0, 0);
       dk[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa_[n % (kAh + 1)], sf[s_], dk[u], 0, 0, 0);
     }
-    stamp(2);
   };
   for (int it = 0; it < nsteps; it += 4) {
     cstep(IC<0>{}, it);
@@ -835,7 +739,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
     cstep(IC<2>{}, it + 2);
     cstep(IC<3>{}, it + 3);
   }
-  stamp_out();
 
   // ---- dK = scale·Σ dS·Q, dV: rows c = 32u + (i&3) + 8(i>>2) + 4h, column = this lane's key
   if (!wave_active || key >= nk) return;
@@ -862,357 +765,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
       if (c < d) dK[(int64_t)c * nk + key] = __float2half(dk[u][i] * sc);
       if (c < vd) dV[(int64_t)c * nk + key] = __float2half(dv[u][i]);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// dK / dV, four roles (D = 128, 16-B aligned shapes; diagnostic build only, FA_BWD_VARIANT=1416:
-// measured slower than the producer / consumer pass).  16 waves: wave w works on key group
-// kg = w & 3 (32 of the workgroup's 128 keys) in role w >> 2, so the four roles of a key group share
-// one SIMD, one wave (128 registers) each:
-//   role 0 (S)   S(i) = Qᵀ·K' (C = -lse2), P(i) = exp2(S), masked  -> P16 and P32 hand-over slots
-//   role 1 (dP)  dS(i-1) = P32(i-1)∘dP(i-1) -> dS hand-over slot; then dP(i) = dOᵀ·V (C = -D), held
-//   role 2 (V)   dV += dO(i-1)·P16(i-1)
-//   role 3 (K)   dK += Q(i-2)·dS(i-2)
-// Each role issues 8 MFMAs a 32-query step (the producer / consumer pass above: 16 + 16 on two
-// waves), and the softmax VALU of one role runs beside the other three's MFMAs.  One barrier a step.
-// The query tiles stream through a 5-slot ring (tile j in slot j % 5: tiles i-2 .. i read, i+1
-// landed, i+2 in flight) by LDS-DMA issued by inline assembly from roles 2 and 3 (two 1-KB blocks a
-// wave a step, hand-counted vmcnt before each barrier).  dS is formed from the fp32 P exactly as in
-// the producer / consumer pass, so the gradients are the same bits.
-struct Q4Smem {
-  static constexpr int D = 128;
-  static constexpr int kBK = 128;                      // keys per workgroup: 4 key groups x 32
-  static constexpr int kRow = D * kBK * 2;             // K (or V) row image (prologue only)
-  static constexpr int kQT = D * 64;                   // one [D][32] Q16 image
-  static constexpr int offQT = 0, offOT = kQT, offLse = 2 * kQT, offD = offLse + 256;
-  static constexpr int kSlot = offLse + 512;           // + -lse2, -D (64-float vectors: DMA lanes)
-  static constexpr int kNS = 5;
-  static constexpr int offP = kNS * kSlot;             // P16: 2 slots x 4 key groups x 2 KB
-  static constexpr int offP32 = offP + 2 * 4 * 2048;   // P32: 2 x 4 x 4 KB
-  static constexpr int offS = offP32 + 2 * 4 * 4096;   // dS16: 2 x 4 x 2 KB
-  static constexpr int kUsed = offS + 2 * 4 * 2048;
-  static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;  // the K/V images alias the ring
-};
-static_assert(Q4Smem::kTotal <= 160 * 1024, "LDS");
-
-template <int POL>
-__global__ __launch_bounds__(1024, 1) void bwd_dkdv_q4_kernel(BwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  lds_char_t* smem = (lds_char_t*)smem_raw;
-  using S = Q4Smem;
-  constexpr int D = S::D, kBK = S::kBK, kThr = 1024;
-
-  const int nq = a.rule.q.n, nk = a.rule.k.n;
-  const uint32_t nkb = (nk + kBK - 1) / kBK;
-  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t bi = bid / nkb;
-  const int k0 = (int)(bid % nkb) * kBK;  // earliest (heaviest under causal) key blocks first
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int role = w >> 2, kg = w & 3;
-  const int h = lane >> 5, r = lane & 31;
-  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
-  const int sig = ((tp & 1) << 1) | (tp >> 1);
-  const float c2 = (float)a.scale * kLog2e;
-
-  const int d = a.d, vd = a.v_d;
-  const __half* K = static_cast<const __half*>(a.K) + bi * (int64_t)d * nk;
-  const __half* V = static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk;
-  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq, 2u * d * nq);
-  const __amdgpu_buffer_rsrc_t ors = make_rsrc(static_cast<const __half*>(a.dO) + bi * (int64_t)vd * nq, 2u * vd * nq);
-  const float* glse = static_cast<const float*>(a.ws_lse) + bi * (int64_t)nq;
-  const float* gD = static_cast<const float*>(a.ws_D) + bi * (int64_t)nq;
-
-  // ---- K, V blocks into LDS (every thread); roles 0 / 1 read their resident B operands below
-  {
-    constexpr int kRPT = 2 * D * (kBK / 8) / kThr, kHalf = D * (kBK / 8) / kThr;
-    static_assert(kHalf * kThr == D * (kBK / 8), "resident chunks must divide over the workgroup");
-    const __amdgpu_buffer_rsrc_t krs2 = make_rsrc(K, 2u * d * nk), vrs2 = make_rsrc(V, 2u * vd * nk);
-    u32x4 rv[kRPT];
-#pragma unroll
-    for (int jj = 0; jj < kRPT; ++jj) {
-      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
-      const int c = j / (kBK / 8), m = j % (kBK / 8);
-      const bool in = c < (which ? vd : d) && k0 + 8 * m < nk;
-      rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? vrs2 : krs2,
-                                                     in ? (uint32_t)c * (uint32_t)nk * 2u + 16u * m : 0x80000000u, 2 * k0, 0);
-    }
-#pragma unroll
-    for (int jj = 0; jj < kRPT; ++jj) {
-      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
-      const int c = j / (kBK / 8), m = j % (kBK / 8);
-      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBK) + ((m * 16) ^ ((c & 3) << 6))) = rv[jj];
-    }
-  }
-  __syncthreads();
-
-  // ---- query range of this key block and the per-lane / per-wave query intervals (every role)
-  const int klast = min(k0 + kBK, nk) - 1;
-  int qb = 0, qe = nq;
-  if (POL != 0) q_range_for_k_block(a.rule, k0, klast, &qb, &qe);
-  const int qt0 = (qb / 32) * 32;
-  const int ntiles = (qe > qb) ? (qe - qt0 + 31) / 32 : 0;
-  const int key = k0 + 32 * kg + r;
-  const int wk0 = k0 + 32 * kg;
-  const bool wave_active = wk0 < nk;
-  int qlo = 0, qspan = nq, wlo_min = 0, wlo_max = 0, whi_min = nq - 1, whi_max = nq - 1;
-  if (POL == 1 && wave_active) {
-    int qhi;
-    query_interval(a.rule, min(key, nk - 1), &qlo, &qhi);
-    qspan = max(qhi - qlo + 1, 0);
-    const int last = min(31, nk - 1 - wk0);
-    wlo_min = __builtin_amdgcn_readfirstlane(qlo);
-    whi_min = __builtin_amdgcn_readfirstlane(qhi);
-    wlo_max = __builtin_amdgcn_readlane(qlo, last);
-    whi_max = __builtin_amdgcn_readlane(qhi, last);
-  }
-  // tile class of tile t (0 skip, 1 edge, 2 interior); tiles outside [0, ntiles) are skipped
-  auto tcls = [&](int t) -> int {
-    if (t < 0 || t >= ntiles || !wave_active) return 0;
-    const int qa = qt0 + 32 * t, qz = qa + 31;
-    if (POL == 0) return 2;  // q >= nq rows: Q = dO = 0 and -lse2 = -D = 0, so their terms vanish
-    if (POL == 2) return qa < nq ? tile_class(a.rule, qa, min(qz, nq - 1), wk0, min(wk0 + 31, nk - 1)) : 0;
-    if (wlo_min > qz || whi_max < qa) return 0;
-    return (wlo_max <= qa && whi_min >= qz) ? 2 : 1;
-  };
-  auto slot = [&](int t) -> const lds_char_t* { return smem + (t % S::kNS) * S::kSlot; };
-  // hand-over addresses of this key group (lane-linear 16-B units)
-  auto xp16 = [&](int t, int j) -> uint32_t { return S::offP + (t & 1) * 8192 + kg * 2048 + j * 1024 + lane * 16; };
-  auto xp32 = [&](int t, int j) -> uint32_t { return S::offP32 + (t & 1) * 16384 + kg * 4096 + j * 1024 + lane * 16; };
-  auto xds = [&](int t, int j) -> uint32_t { return S::offS + (t & 1) * 8192 + kg * 2048 + j * 1024 + lane * 16; };
-
-  // ---- LDS-DMA staging (roles 2, 3: stager sx = 4 (role - 2) + kg issues 1-KB blocks 2sx, 2sx+1 of
-  // a tile; blocks 0-7 the Q16 image, 8-15 the dO16 image, block b = channel rows 16b .. 16b+15,
-  // lane L = row 16b + L/4, position L%4 = source chunk (L%4) ^ swizzle(row)); stager 0 also moves
-  // -lse2 / -D of queries qa .. qa+63 by two dword LDS-DMAs.  Past nq these read 0, which is safe:
-  // those queries' Q and dO are zero as well, so S = dP = D = 0, P = 1 and every term they feed
-  // (dO·P, Q·dS with dS = P·(dP - D)) vanishes.
-  const int sx = 4 * (role - 2) + kg;
-  uint32_t dvoff[2];
-  int dcm[2];
-  const __amdgpu_buffer_rsrc_t lrs = make_rsrc(glse, 4u * nq), drs = make_rsrc(gD, 4u * nq);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int blk = 2 * sx + j, b = blk & 7, row = 16 * b + (lane >> 2);
-    dcm[j] = (lane & 3) ^ ((row >> 2) & 3);
-    dvoff[j] = row < (blk >= 8 ? vd : d) ? (uint32_t)row * (uint32_t)nq * 2u + 16u * dcm[j] : 0x80000000u;
-  }
-  auto dma_tile = [&](int t) __attribute__((always_inline)) {
-    const int qa = qt0 + 32 * t;
-    const uint32_t sb = (uint32_t)(uintptr_t)(smem + (t % S::kNS) * S::kSlot);
-    if (sx == 0) {
-      const uint32_t off = qa + lane < nq ? 4u * (uint32_t)lane : 0x80000000u;
-      asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
-                   :
-                   : "v"(off), "s"(lrs), "s"(4 * min(qa, nq)), "{m0}"(sb + (uint32_t)S::offLse)
-                   : "memory");
-      asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
-                   :
-                   : "v"(off), "s"(drs), "s"(4 * min(qa, nq)), "{m0}"(sb + (uint32_t)S::offD)
-                   : "memory");
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int blk = 2 * sx + j;
-      const uint32_t m0v = sb + (uint32_t)((blk >= 8 ? S::offOT : S::offQT) + (blk & 7) * 1024);
-      const uint32_t vo = qa + 8 * dcm[j] < nq ? dvoff[j] : 0x80000000u;
-      // (s_nop 0: the wait state between the SALU write of M0 and the LDS-DMA that reads it)
-      asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
-                   :
-                   : "v"(vo), "s"(blk >= 8 ? ors : qrs), "s"(2 * min(qa, nq)), "{m0}"(m0v)
-                   : "memory");
-    }
-  };
-  // steps it = 0 .. ntiles + 1: roles 0 / 1 on tile it, role 2 on tile it-1, role 3 on tile it-2
-  const int nsteps = ntiles + 2;
-  auto step_head = [&](int it) __attribute__((always_inline)) {
-    // stagers: all but this wave's most recent step of DMAs done (tile it has landed)
-    if (role >= 2) {
-      if (sx == 0) __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4)
-      else __builtin_amdgcn_s_waitcnt(0x0F72);          // vmcnt(2)
-    }
-    __syncthreads();
-    if (role >= 2) dma_tile(it + 2);  // into the slot of tile it-3 (its last reader, role 3, ran at it-1)
-  };
-  // the K/V images alias the ring: roles 0 / 1 read their operands, then the first two tiles go in
-  auto prologue_dma = [&]() __attribute__((always_inline)) {
-    __syncthreads();
-    if (role >= 2) {
-      dma_tile(0);
-      dma_tile(1);
-    }
-  };
-
-  if (role <= 1) {
-    // ================= roles 0 (S) and 1 (dP): resident B operand X[c = 16s + 8h + j][key]
-    half8 xb[D / 16];
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int crow = 16 * s + 8 * (g >> 1) + 4 * e + tq;
-        const int col = 32 * kg + 16 * (g & 1) + 4 * tp;
-        const uint32_t off = crow * (2 * kBK) + ((col * 2) ^ ((crow & 3) << 6));
-        const half4 x = tr_read(smem + role * S::kRow + off);
-        if (e == 0) xb[s].lo = x; else xb[s].hi = x;
-      }
-    if (role == 0) {
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) xb[s] = scale8(xb[s], c2);  // S in log2 units straight out of the MFMA
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every image read done before the ring reuses it
-    prologue_dma();
-    const int ko = (POL == 2) ? seq_order(a.rule.k, a.rule, min(key, nk - 1)) : 0;
-    // this role's accumulator over tile t: C = the row constant (registers 4gq..4gq+3 = queries
-    // 16(gq>>1) + 8h + 4(gq&1) + 0..3), A = transposed reads of the Q16 (role 0) / dO16 image
-    auto product = [&](int t, floatx16& acc) __attribute__((always_inline)) {
-      const lds_char_t* base = slot(t);
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int q4 = 16 * (gq >> 1) + 8 * h + 4 * (gq & 1);
-        const floatx4 c4 = *reinterpret_cast<const lds_f4_t*>(base + (role == 0 ? S::offLse : S::offD) + 4 * q4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[4 * gq + j] = c4[j];
-      }
-      const lds_char_t* img = base + (role == 0 ? S::offQT : S::offOT);
-      constexpr int kS = D / 16, kAh = 2;
-      half8 op[kAh + 1];
-      auto rd = [&](int s_) __attribute__((always_inline)) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const uint32_t off = q16_off(16 * s_ + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
-          const half4 x = tr_read(img + off);
-          if (e == 0) op[s_ % (kAh + 1)].lo = x; else op[s_ % (kAh + 1)].hi = x;
-        }
-      };
-#pragma unroll
-      for (int s_ = 0; s_ < kAh; ++s_) rd(s_);
-#pragma unroll
-      for (int s_ = 0; s_ < kS; ++s_) {
-        if (s_ + kAh < kS) rd(s_ + kAh);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(op[s_ % (kAh + 1)], xb[s_], acc, 0, 0, 0);
-      }
-    };
-    if (role == 0) {
-      for (int it = 0; it < nsteps; ++it) {
-        step_head(it);
-        const int cls = tcls(it);
-        if (cls == 0) continue;
-        floatx16 sacc;
-        product(it, sacc);
-        const int qa = qt0 + 32 * it;
-        // P = exp2(S); register i = query 16(i>>3) + 8h + (i&7) = k-step i>>3 of roles 2 / 3
-        half8 pf[2];
-        auto softmax = [&](bool masked) __attribute__((always_inline)) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            float pv = __builtin_amdgcn_exp2f(sacc[i]);
-            if (POL == 1 && masked) {
-              const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
-              pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
-            }
-            if (POL == 2 && masked) {
-              const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
-              pv = (q < nq && check_orders_bf(a.rule, seq_order(a.rule.q, a.rule, min(q, nq - 1)), ko)) ? pv : 0.f;
-            }
-            sacc[i] = pv;
-            pf[i >> 3][i & 7] = (_Float16)pv;
-          }
-        };
-        if (POL != 0 && cls == 1) {  // the edge mask as a real branch (see the producer above)
-          asm volatile("; edge tile" ::: );
-          softmax(true);
-        } else {
-          asm volatile("; interior tile" ::: );
-          softmax(false);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) *reinterpret_cast<lds_half8_t*>(smem + xp16(it, j)) = pf[j];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          *reinterpret_cast<lds_f4_t*>(smem + xp32(it, j)) = floatx4{sacc[4 * j], sacc[4 * j + 1], sacc[4 * j + 2], sacc[4 * j + 3]};
-      }
-      return;
-    }
-    // role 1
-    floatx16 pacc;
-    for (int it = 0; it < nsteps; ++it) {
-      step_head(it);
-      if (tcls(it - 1) != 0) {  // dS(it-1) = P(it-1)∘(dP(it-1) - D), the producer / consumer pass's rounding
-        half8 sf[2];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const floatx4 p4 = *reinterpret_cast<const lds_f4_t*>(smem + xp32(it - 1, j));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int i = 4 * j + e;
-            sf[i >> 3][i & 7] = (_Float16)(p4[e] * pacc[i]);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) *reinterpret_cast<lds_half8_t*>(smem + xds(it - 1, j)) = sf[j];
-      }
-      if (tcls(it) != 0) product(it, pacc);
-    }
-    return;
-  }
-
-  // ================= roles 2 (dV) and 3 (dK)
-  prologue_dma();
-  floatx16 acc[D / 32];
-#pragma unroll
-  for (int u = 0; u < D / 32; ++u)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[u][i] = 0.f;
-  const int lag = role - 1;  // role 2 works on tile it-1, role 3 on tile it-2
-  for (int it = 0; it < nsteps; ++it) {
-    step_head(it);
-    const int t = it - lag;
-    if (tcls(t) == 0) continue;
-    const lds_char_t* img = slot(t) + (role == 2 ? S::offOT : S::offQT);
-    half8 bf[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) bf[j] = read_b128(smem + (role == 2 ? xp16(t, j) : xds(t, j)));
-    // A = X[row 32u + r][queries 16s + 8h + 0..7] (b128 reads, two ahead)
-    constexpr int kU = D / 32, kN = 2 * kU, kAh = 2;
-    half8 xa[kAh + 1];
-    auto rd = [&](int n) __attribute__((always_inline)) {
-      const int s_ = n / kU, u = n % kU;
-      xa[n % (kAh + 1)] = read_b128(img + q16_off(32 * u + r, 2 * s_ + h));
-    };
-#pragma unroll
-    for (int n = 0; n < kAh; ++n) rd(n);
-#pragma unroll
-    for (int n = 0; n < kN; ++n) {
-      if (n + kAh < kN) rd(n + kAh);
-      const int s_ = n / kU, u = n % kU;
-      acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[n % (kAh + 1)], bf[s_], acc[u], 0, 0, 0);
-    }
-  }
-  // ---- dK = scale·Σ dS·Q (role 3), dV (role 2): rows c = 32u + (i&3) + 8(i>>2) + 4h, this lane's key
-  if (!wave_active || key >= nk) return;
-  const float sc = role == 3 ? (float)a.scale : 1.f;
-  __half* X = static_cast<__half*>(role == 3 ? a.dK : a.dV) + bi * (int64_t)(role == 3 ? d : vd) * nk;
-  const int xd = role == 3 ? d : vd;
-  if (xd == D) {
-    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(X, 2u * xd * nk);
-    const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nk + (uint32_t)key);
-#pragma unroll
-    for (int u = 0; u < D / 32; ++u)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t so = 2u * (32u * u + (i & 3) + 8u * (i >> 2)) * (uint32_t)nk;
-        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(acc[u][i] * sc)), xrs, vlane, so, 0);
-      }
-    return;
-  }
-#pragma unroll
-  for (int u = 0; u < D / 32; ++u)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-      if (c < xd) X[(int64_t)c * nk + key] = __float2half(acc[u][i] * sc);
     }
 }
 
@@ -1568,26 +1120,11 @@ struct DqPcSmem {
   static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;  // the Q/dO images alias the ring
 };
 
-template <int D, int POL, bool ALN, int PF = 0>
+template <int D, int POL, bool ALN>
 __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
   using S = DqPcSmem<D>;
-  // PF & 4 (diagnostic build): per-wave s_memtime sums of each step's parts, written to the unused
-  // dQ workspace (producer: barrier, half-0 MFMAs, half-0 softmax, half-1 MFMAs, half-1 softmax;
-  // consumer: barrier, staging, hand-over reads, MFMAs)
-  constexpr bool STAMP = (PF & 4) != 0;
-  uint64_t stv[5] = {0, 0, 0, 0, 0}, st_prev = 0;
-  auto stamp = [&](int k) __attribute__((always_inline)) {
-    if constexpr (STAMP) {
-      __builtin_amdgcn_sched_barrier(0);
-      uint64_t t;
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      if (k >= 0) stv[k] += t - st_prev;
-      st_prev = t;
-    }
-  };
   constexpr int kThr = 512, kHalfThr = 256;  // one half of the workgroup stages
   constexpr int kBM = S::kBM, kBN = 64;
   constexpr int kKChunks = D * 8;  // 16-B chunks of one [D][64] tile
@@ -1606,17 +1143,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
   const int h = lane >> 5, r = lane & 31;
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const float c2 = (float)a.scale * kLog2e;
-  auto stamp_out = [&]() __attribute__((always_inline)) {
-    if constexpr (STAMP) {
-      if (lane < 5) {
-        uint64_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) v = (lane == k) ? stv[k] : v;
-        reinterpret_cast<uint64_t*>(a.ws_dQ)[((int64_t)bid * 8 + w) * 8 + lane] = v;
-      }
-    }
-  };
-
   const int d = a.d, vd = a.v_d;
   const __half* Q = static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq;
   const __half* dO = static_cast<const __half*>(a.dO) + bi * (int64_t)vd * nq;
@@ -1805,9 +1331,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
       __syncthreads();  // (stage0 of the consumers)
       auto pstep = [&](auto C_, int it) __attribute__((always_inline)) {
         constexpr int c = decltype(C_)::value;
-        stamp(-1);
         __syncthreads();
-        stamp(0);
         const int ka = kt0 + it * kBN;
         const int cls = it < ntiles ? tcls(ka) : 0;
         if (cls == 0) return;
@@ -1816,7 +1340,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
         for (int t = 0; t < 2; ++t) {  // one 32-key half at a time: 16 MFMAs, then its two dSᵀ k-steps
           const floatx16 st = half_chain(base + S::offKT, qf, negl, t);
           const floatx16 dp = half_chain(base + S::offVT, of, negd, t);
-          stamp(1 + 2 * t);
           auto softmax = [&](int cl) __attribute__((always_inline)) {
 #pragma unroll
             for (int sh = 0; sh < 2; ++sh) {
@@ -1834,7 +1357,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
             asm volatile("; interior tile" ::: );
             softmax(2);
           }
-          stamp(2 + 2 * t);
         }
       };
       for (int it = 0; it < nsteps; it += 4) {
@@ -1843,7 +1365,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
         pstep(IC<2>{}, it + 2);
         pstep(IC<3>{}, it + 3);
       }
-      stamp_out();
       return;
     }
   }
@@ -1869,7 +1390,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
     half8 dsf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) dsf[s] = read_b128(smem + xoff((c + 1) % 2, s));
-    stamp(2);
     constexpr int kN = 4 * (D / 32);
     half8 ka8p[3];
     auto rka = [&](int n) __attribute__((always_inline)) {  // operand n = (D/32)·s + u, two ahead
@@ -1889,14 +1409,10 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
   // stay exact), then dQ += K·dSᵀ of tile it-1
   auto cstep = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;
-    stamp(-1);
     __syncthreads();
-    stamp(0);
     store_tile((c + 1) % 4, (c + 1) % 2);
     load_tile(kt0 + kBN * (it + 3), (c + 1) % 2);
-    stamp(1);
     cwork(C_, it);
-    stamp(3);
   };
   for (int it = 0; it < nsteps; it += 4) {
     cstep(IC<0>{}, it);
@@ -1904,7 +1420,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_pc_kernel(BwdArgs a) {
     cstep(IC<2>{}, it + 2);
     cstep(IC<3>{}, it + 3);
   }
-  stamp_out();
 
   if (!wave_active || qi >= nq) return;
   __half* dQ = static_cast<__half*>(a.dQ) + bi * (int64_t)d * nq;
@@ -1958,36 +1473,22 @@ hipError_t launch_dkdv(const BwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int D, int PF = 0>
+template <int D>
 hipError_t launch_dkdv_pc(const BwdArgs& a, hipStream_t s) {
   using S = PcSmem<D>;
   const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
   const int pol = bwd_pol(a.rule);
-  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dkdv_pc_kernel<D, 0, true, PF>
-                                           : pol == 1 ? bwd_dkdv_pc_kernel<D, 1, true, PF>
-                                                      : bwd_dkdv_pc_kernel<D, 2, true, PF>)
-                                        : (pol == 0   ? bwd_dkdv_pc_kernel<D, 0, false, PF>
-                                           : pol == 1 ? bwd_dkdv_pc_kernel<D, 1, false, PF>
-                                                      : bwd_dkdv_pc_kernel<D, 2, false, PF>);
+  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dkdv_pc_kernel<D, 0, true>
+                                           : pol == 1 ? bwd_dkdv_pc_kernel<D, 1, true>
+                                                      : bwd_dkdv_pc_kernel<D, 2, true>)
+                                        : (pol == 0   ? bwd_dkdv_pc_kernel<D, 0, false>
+                                           : pol == 1 ? bwd_dkdv_pc_kernel<D, 1, false>
+                                                      : bwd_dkdv_pc_kernel<D, 2, false>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(512), S::kTotal, s, a);
   return hipGetLastError();
 }
-
-#ifdef FA_DIAG
-// the four-role dK/dV pass (D = 128, 16-B aligned shapes; diagnostic variant 1416, not taken)
-hipError_t launch_dkdv_q4(const BwdArgs& a, hipStream_t s) {
-  using S = Q4Smem;
-  const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
-  const int pol = bwd_pol(a.rule);
-  const BwdKernel kern = pol == 0 ? bwd_dkdv_q4_kernel<0> : pol == 1 ? bwd_dkdv_q4_kernel<1> : bwd_dkdv_q4_kernel<2>;
-  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(1024), S::kTotal, s, a);
-  return hipGetLastError();
-}
-#endif
 
 template <int D, int NW, int WPE, bool PRE = false, bool MSPEC = false>
 hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
@@ -2035,17 +1536,17 @@ hipError_t launch_bwd_wide(const BwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int D, int PF = 0>
+template <int D>
 hipError_t launch_dq_pc(const BwdArgs& a, hipStream_t s) {
   using S = DqPcSmem<D>;
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
   const int pol = bwd_pol(a.rule);
-  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_pc_kernel<D, 0, true, PF>
-                                           : pol == 1 ? bwd_dq_pc_kernel<D, 1, true, PF>
-                                                      : bwd_dq_pc_kernel<D, 2, true, PF>)
-                                        : (pol == 0   ? bwd_dq_pc_kernel<D, 0, false, PF>
-                                           : pol == 1 ? bwd_dq_pc_kernel<D, 1, false, PF>
-                                                      : bwd_dq_pc_kernel<D, 2, false, PF>);
+  const BwdKernel kern = bwd_aligned(a) ? (pol == 0   ? bwd_dq_pc_kernel<D, 0, true>
+                                           : pol == 1 ? bwd_dq_pc_kernel<D, 1, true>
+                                                      : bwd_dq_pc_kernel<D, 2, true>)
+                                        : (pol == 0   ? bwd_dq_pc_kernel<D, 0, false>
+                                           : pol == 1 ? bwd_dq_pc_kernel<D, 1, false>
+                                                      : bwd_dq_pc_kernel<D, 2, false>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(512), S::kTotal, s, a);
@@ -2078,10 +1579,9 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   if (max(a.d, a.v_d) > 128) return launch_bwd_wide(a, s);
 #ifdef FA_DIAG
   // FA_BWD_VARIANT (diagnostic library): d <= 64 — 82 eight-wave blocks, 1068 / 1069 the dQ pass's
-  // operand reads run ahead, 1071 its edge mask as a branch; d = 128 — 1404 the dK/dV pass's stamp
-  // build (tools/pc_stamps.py), 1599 the one-wave dQ pass (the unaligned shapes' structure) on
-  // aligned shapes, 1604 the producer / consumer dQ pass's stamp build (tools/dq_stamps.py).  The
-  // rest of round 2's and round 3's A/B variants were measured and removed.
+  // operand reads run ahead, 1071 its edge mask as a branch; d = 128 — 1599 the one-wave dQ pass (the
+  // unaligned shapes' structure) on aligned shapes.  The other A/B variants of rounds 2-4 (stamp
+  // builds, LDS-DMA staging, the four-role dK/dV pass) were measured and removed.
   const int v = diag_variant("FA_BWD_VARIANT");
   if (max(a.d, a.v_d) <= 64 && v >= 0) {
     e = v == 82 ? launch_dkdv<64, 8, 2>(a, s) : launch_dkdv<64, 4, 2>(a, s);
@@ -2094,13 +1594,9 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
     }
   }
   if (max(a.d, a.v_d) > 64 && v >= 0) {
-    e = v == 1404   ? launch_dkdv_pc<128, 4>(a, s)
-        : v == 1408 ? launch_dkdv_pc<128, 8>(a, s)
-        : (v == 1416 && bwd_aligned(a)) ? launch_dkdv_q4(a, s)
-                    : launch_dkdv_pc<128>(a, s);
+    e = launch_dkdv_pc<128>(a, s);
     if (e != hipSuccess) return e;
     if (v == 1599 || !bwd_aligned(a)) return launch_dq<128, 4, 1, true>(a, s);
-    if (v == 1604) return launch_dq_pc<128, 4>(a, s);  // stamp build (tools/dq_stamps.py)
     return launch_dq_pc<128>(a, s);
   }
 #endif
