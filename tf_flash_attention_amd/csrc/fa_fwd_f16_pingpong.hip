@@ -34,6 +34,7 @@
 #include "fa_device.h"
 #include "fa_kernels.h"
 #include "fa_mfma.h"
+#include "fa_softmax_stream.h"
 
 namespace fa {
 namespace {
@@ -104,6 +105,9 @@ constexpr int kFHalfMax = 1048576;
 // tiles of the current epoch (fp16 rounding of P: |error| <= 2^-11 log2(e) in log2 units, i.e.
 // < 4.9e-4 in m), exact for the tiles that rebased.
 constexpr int kFPMax = 1 << 22;
+// the exp2 / pack / packed-max part of the softmax as a hand-ordered stream (fa_softmax_stream.h):
+// conversions one pair (kFAsmSm) or two pairs (kFAsmSm2) behind their exponentials
+constexpr int kFAsmSm = 1 << 25, kFAsmSm2 = 1 << 26;
 
 template <int POL, int F>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a) {
@@ -423,11 +427,18 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   };
   auto softmax_p = [&](int it, int cls) __attribute__((always_inline)) {
     if (cls == 1) mask(kt0 + it * kBN);
-    exp_cvt();
+    half2v tm;
+    if constexpr ((F & (kFAsmSm | kFAsmSm2)) != 0) {
+      uint32_t pm;
+      softmax_stream_tile<(F & kFAsmSm2) ? 2 : 1>(st, pw, pm);
+      tm = __builtin_bit_cast(half2v, pm);
+    } else {
+      exp_cvt();
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
-      asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
-    const half2v tm = pmax_tile();
+      for (int x = 0; x < 4; ++x)
+        asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
+      tm = pmax_tile();
+    }
     const _Float16 tmx = __builtin_elementwise_maximum(tm[0], tm[1]);
     const half2v pmr_old = pmr;
     pmr = __builtin_elementwise_maximum(pmr, tm);
@@ -872,6 +883,8 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2297: return launch_t<kFDefault | kANoExp>(a, s);             // timing only: no exp2 (outputs wrong)
     case 2298: return launch_t<kFDefault | kANoLoad | kANoStore>(a, s);  // timing only: no staging
     case 2299: return launch_t<kFDefault | kFStamp>(a, s);
+    case 2240: return launch_t<kFDefault | kFAsmSm>(a, s);
+    case 2241: return launch_t<kFDefault | kFAsmSm2>(a, s);
     default: break;
   }
 #endif
