@@ -37,6 +37,7 @@
 #include "fa_device.h"
 #include "fa_kernels.h"
 #include "fa_mfma.h"
+#include "fa_softmax_stream.h"
 
 #include <string.h>
 
@@ -107,6 +108,9 @@ constexpr int kBANoDmaWait = 8192;
 constexpr int kBMaskPk = 16384;
 // (with kBMaskPk) the pairs as two independent chains of eight, one per 32-key half
 constexpr int kBMaskPk2 = 32768;
+// the exp2 / pack / packed-max part of a non-first tile's softmax as the hand-ordered stream of
+// fa_softmax_stream.h (the conversions one pair behind their exponentials)
+constexpr int kBAsmSm = 65536;
 constexpr int kBandR3Final = kBFPMax | kBStag | kBEpiSplit;  // round 3: staggered groups, split epilogue
 // round 4: + exponentials in batches (c4, one process: 4.109-4.147 against 4.139-4.194 ms; outputs
 // bitwise unchanged)
@@ -618,11 +622,18 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     } else if constexpr (PMAX) {
       // the rebase check on the packed P (fa_fwd_f16_pingpong.hip, kFPMax): the exponentials run
       // against m_run anyway; the exact fp32 max is formed only in the (rare) rebase branch
-      exp_cvt();
+      half2v tm;
+      if constexpr ((F & kBAsmSm) != 0) {
+        uint32_t pm;
+        softmax_stream_tile<1>(st, pw, pm);
+        tm = __builtin_bit_cast(half2v, pm);
+      } else {
+        exp_cvt();
 #pragma unroll
-      for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
-        asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
-      const half2v tm = pmax_tile();
+        for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
+          asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
+        tm = pmax_tile();
+      }
       const _Float16 tmx = __builtin_elementwise_maximum(tm[0], tm[1]);
       const half2v pmr_old = pmr;
       pmr = __builtin_elementwise_maximum(pmr, tm);
@@ -1204,6 +1215,7 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   if (dv == 2431 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBDma | kBANoDmaWait>(ba, s);
   if (dv == 2432 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBMaskPk>(ba, s);
   if (dv == 2433 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBMaskPk | kBMaskPk2>(ba, s);
+  if (dv == 2440 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBAsmSm>(ba, s);
 #endif
   switch (ba.T) {
     case 10: return launch_band_t<10>(ba, s);
