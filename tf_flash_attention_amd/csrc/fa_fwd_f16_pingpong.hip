@@ -885,6 +885,7 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s) {
     case 2299: return launch_t<kFDefault | kFStamp>(a, s);
     case 2240: return launch_t<kFDefault | kFAsmSm>(a, s);
     case 2241: return launch_t<kFDefault | kFAsmSm2>(a, s);
+    case 2242: return launch_t<kFDefault | kFAsmSm | kFStamp>(a, s);
     default: break;
   }
 #endif
