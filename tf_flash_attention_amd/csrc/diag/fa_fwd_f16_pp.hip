@@ -26,6 +26,9 @@
 //     the 64 banks).
 // One barrier per key tile.  Staging is register-based (global → registers two
 // steps ahead → LDS); tiles i+2 (K) / i+1 (V) are already resident when tile i runs.
+// Round 5: the K / V fragments are double-buffered (by step parity, 4-slot rings): step i reads
+// K(i+2) in its first segment and V(i+1) in its second into the buffers the next step uses, so no
+// segment starts behind an LDS round trip.
 //
 // Numerics are those of fa_fwd_f16.hip / fa_fwd_f16_fast.hip (fp32 accumulation,
 // log2-domain lazy rebase with threshold 8, l relative to the stored fp16 m).
@@ -44,7 +47,7 @@ constexpr int kD = 64;
 constexpr int kBN = 64;                 // keys per tile
 constexpr int kNW = 4;                  // waves per workgroup (one per SIMD)
 constexpr int kBM = 64 * kNW;           // queries per workgroup
-constexpr int kNS = 3;                  // ring slots for K and for V
+constexpr int kNS = 4;                  // ring slots for K and for V
 constexpr int kQRow = 2 * kBM;          // bytes per Q row in LDS
 constexpr int kTile = kD * kBN * 2;     // 8 KB
 constexpr int kOffK = kD * kQRow;       // Q image [64][256] first (prologue only)
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_pp_kernel(FwdArgs a) {
 #pragma unroll
     for (int j = 0; j < kCPT; ++j) *reinterpret_cast<lds_u32x4_t*>(smem + off + wo[j]) = src[j];
   };
-  // staging buffers: buffer j holds K(i+3) / V(i+2) for the step i with i mod 3 == j; loads
+  // staging buffers: buffer j holds K(i+3) / V(i+2) for the step i with i mod kNS == j; loads
   // are issued two steps before their store
   u32x4 kr[kNS][kCPT], vr[kNS][kCPT];
 
@@ -230,32 +233,32 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_pp_kernel(FwdArgs a) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) vbase[s] = r * 128 + 16 * ((2 * s + h) ^ ((r >> 1) & 7));
 
-  half8 kf[2][4];  // K fragments of the tile whose Sᵀ is being issued
-  half8 vf[4][2];  // V fragments of the tile whose PV is being issued
-  auto read_k = [&](int slot) {
+  half8 kf[2][2][4];  // K fragments (two buffers, by step parity)
+  half8 vf[2][4][2];  // V fragments (two buffers, by step parity)
+  auto read_k = [&](int slot, int bf) {
     const lds_char_t* p = smem + kOffK + slot * kTile;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        kf[t][s].lo = tr_read(p + kbase[t] + (16 * s) * 128);
-        kf[t][s].hi = tr_read(p + kbase[t] + (16 * s + 4) * 128);
+        kf[bf][t][s].lo = tr_read(p + kbase[t] + (16 * s) * 128);
+        kf[bf][t][s].hi = tr_read(p + kbase[t] + (16 * s + 4) * 128);
       }
   };
-  auto read_v = [&](int slot) {
+  auto read_v = [&](int slot, int bf) {
     const lds_char_t* p = smem + kOffV + slot * kTile;
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) vf[s][u] = read_b128(p + vbase[s] + 32 * u * 128);
+      for (int u = 0; u < 2; ++u) vf[bf][s][u] = read_b128(p + vbase[s] + 32 * u * 128);
   };
-  // Sᵀ MFMAs of k-steps [s0, s1) for block X
-  auto qk = [&](Blk& X, int s0, int s1) {
+  // Sᵀ MFMAs of k-steps [s0, s1) for block X (K fragments of buffer bf)
+  auto qk = [&](Blk& X, int s0, int s1, int bf) {
 #pragma unroll
     for (int s = s0; s < s1; ++s)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        X.st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][s], X.qf[s], s == 0 ? X.negm : X.st[t], 0, 0, 0);
+        X.st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[bf][t][s], X.qf[s], s == 0 ? X.negm : X.st[t], 0, 0, 0);
   };
   // per-element rule / tail mask of a mixed tile; the key offset inside the tile is an immediate
   auto mask = [&](Blk& X, int k0) {
@@ -352,13 +355,13 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_pp_kernel(FwdArgs a) {
       exp_cvt(X);
     }
   };
-  auto pv = [&](Blk& X, int s0, int s1) {
+  auto pv = [&](Blk& X, int s0, int s1, int bf) {
 #pragma unroll
     for (int s = s0; s < s1; ++s)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const half8 p = __builtin_bit_cast(half8, u32x4{X.pw[s][0], X.pw[s][1], X.pw[s][2], X.pw[s][3]});
-        X.o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[s][u], p, X.o[u], 0, 0, 0);
+        X.o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[bf][s][u], p, X.o[u], 0, 0, 0);
       }
   };
 
@@ -367,22 +370,22 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_pp_kernel(FwdArgs a) {
     return k0 >= kt0 + ntiles * kBN || tcls(X, k0) != 2;
   };
 
-  // ---- prologue compute: Sᵀ(0) of both blocks, softmax of A(0)
+  // ---- prologue compute: Sᵀ(0) of both blocks, softmax of A(0); K(1) and V(0) fragments
   if (ntiles > 0) {
-    read_k(0);
-    qk(A, 0, 4);
-    qk(B, 0, 4);
-    read_k(1);  // (stale when ntiles == 1: a phantom tile, fully masked)
-    read_v(0);
+    read_k(0, 0);
+    qk(A, 0, 4, 0);
+    qk(B, 0, 4, 0);
+    read_k(1, 1);  // (stale when ntiles == 1: a phantom tile, fully masked)
+    read_v(0, 0);
     if (need_mask(A, kt0)) mask(A, kt0);
     softmax(A);
     row_sums(A);
   }
 
-  // ---- step i (slot c = i mod 3): K(i+1) and V(i) fragments are in registers on entry.
-  // Every step has the same straight-line shape: tiles a rule leaves partly (or wholly)
-  // disallowed for a block are masked in a rare uniform branch, and the last step issues a
-  // phantom Sᵀ for tile i+1 (stale LDS, fully masked, never multiplied into O).
+  // ---- step i (ring slot c = i mod 4, fragment buffer p = i mod 2): K(i+1) fragments are in kf[p ^ 1],
+  // V(i) fragments in vf[p] on entry.  Every step has the same straight-line shape: tiles a rule leaves
+  // partly (or wholly) disallowed for a block are masked in a rare uniform branch, and the last step
+  // issues a phantom Sᵀ for tile i+1 (stale LDS, fully masked, never multiplied into O).
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
   auto stamp = [&](int k) {
     if constexpr ((ABL & kAStamp) != 0) {
@@ -395,50 +398,50 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_pp_kernel(FwdArgs a) {
     }
   };
   auto step = [&](auto C_, int it) {
-    constexpr int c = decltype(C_)::value;
+    constexpr int c = decltype(C_)::value, p = c & 1;
     stamp(-1);
     if (!(ABL & kANoBar)) __builtin_amdgcn_s_barrier();
     stamp(0);
     const int k0 = kt0 + it * kBN;
-    // Stores and loads are spread over the step's four scheduling regions (the vector-memory
-    // path of a CU is shared by its four waves; bunched after the barrier they queue).
     // Stores are unconditional: past the end they write zeros into slots nobody reads unmasked.
 
-    // segment 2i: Sᵀ A(i+1) | softmax B(i) | PV A(i)
+    // segment 2i: Sᵀ A(i+1) | softmax B(i) | PV A(i); K(i+2) fragments into the other buffer
     if (need_mask(B, k0)) mask(B, k0);
     stamp(1);
-    store_tile(kOffK + c * kTile, kwo, kr[c]);  // K(i+3) over K(i)
+    store_tile(kOffK + ((c + 3) % kNS) * kTile, kwo, kr[c]);  // K(i+3) over K(i-1)
     if (!(ABL & kANoLoad)) load_chunk(kr[(c + 2) % kNS], 0, krs, koff, kt0 + (it + 5) * kBN);
-    qk(A, 0, 4);
-    pv(A, 0, 2);
+    qk(A, 0, 4, p ^ 1);
+    pv(A, 0, 2, p);
     softmax(B);
     stamp(2);
     if (!(ABL & kANoLoad)) load_chunk(kr[(c + 2) % kNS], 1, krs, koff, kt0 + (it + 5) * kBN);
+    if (!(ABL & kANoFrag)) read_k((c + 2) % kNS, p);
     row_sums(B);
-    pv(A, 2, 4);
+    pv(A, 2, 4, p);
     stamp(3);
 
-    // segment 2i+1: Sᵀ B(i+1) | softmax A(i+1) | PV B(i); then K(i+2), V(i+1) fragments
+    // segment 2i+1: Sᵀ B(i+1) | softmax A(i+1) | PV B(i); V(i+1) fragments into the other buffer
     if (need_mask(A, k0 + kBN)) mask(A, k0 + kBN);
-    store_tile(kOffV + ((c + 2) % kNS) * kTile, vwo, vr[c]);  // V(i+2) over V(i-1)
+    store_tile(kOffV + ((c + 2) % kNS) * kTile, vwo, vr[c]);  // V(i+2) over V(i-2)
     if (!(ABL & kANoLoad)) load_chunk(vr[(c + 2) % kNS], 0, vrs, voffs, kt0 + (it + 4) * kBN);
-    qk(B, 0, 4);
-    pv(B, 0, 2);
+    qk(B, 0, 4, p ^ 1);
+    pv(B, 0, 2, p);
     softmax(A);
     stamp(4);
     if (!(ABL & kANoLoad)) load_chunk(vr[(c + 2) % kNS], 1, vrs, voffs, kt0 + (it + 4) * kBN);
-    if (!(ABL & kANoFrag)) read_k((c + 2) % kNS);
     row_sums(A);
-    pv(B, 2, 4);
-    // this step's LDS stores are complete before any wave reaches the next barrier
+    pv(B, 2, 4, p);
+    // this step's LDS stores are complete before any wave reaches the next barrier; the V(i+1)
+    // reads (for the next step's PVs, a segment of Sᵀ MFMAs later) go after that wait
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    if (!(ABL & kANoFrag)) read_v((c + 1) % kNS);
+    if (!(ABL & kANoFrag)) read_v((c + 1) % kNS, p ^ 1);
     stamp(5);
   };
   for (int it = 0; it < ntiles; it += kNS) {
     step(IC<0>{}, it);
     if (it + 1 < ntiles) step(IC<1>{}, it + 1);
     if (it + 2 < ntiles) step(IC<2>{}, it + 2);
+    if (it + 3 < ntiles) step(IC<3>{}, it + 3);
   }
 
   // ---- epilogue

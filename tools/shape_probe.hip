@@ -12,6 +12,8 @@
 //   mode 0: 32x32x16 beside the softmax      mode 1: 16x16x32 beside the softmax
 //   mode 2: 32x32x16, partner idle           mode 3: 16x16x32, partner idle
 //   mode 4: softmax, partner idle
+//   mode 11: 32x32x16 with the Sᵀ and PV chains interleaved (four chains in flight) beside the softmax;
+//   mode 12: the same, partner idle
 //   modes 5-10: the softmax as a hand-ordered asm stream (tools/gen/softmax_stream.py): lag 1 / dlag 1
 //   alone (5) and beside 32x32x16 (6); lag 2 alone (7) and beside (8); dlag 2 alone (9) and beside (10)
 // Prints cycles per interval, the in-kernel clock, the MFMA TF/s and the softmax wave's own cycles
@@ -71,9 +73,9 @@ __global__ __launch_bounds__(512, 1) void probe(unsigned long long* out, float* 
   for (int i = 0; i < 32; ++i) s[i] = -(float)((tid * 37 + i * 11) % 97) * 0.09f;
   float l[4] = {0.f, 0.f, 0.f, 0.f};
   uint32_t pm = 0;
-  constexpr bool ASM = MODE >= 5;
+  constexpr bool ASM = MODE >= 5 && MODE <= 10;
   constexpr int LAG = (MODE == 7 || MODE == 8) ? 2 : 1, DLAG = (MODE == 9 || MODE == 10) ? 2 : 1;
-  const bool do_mfma = (MODE != 4 && MODE != 5 && MODE != 7 && MODE != 9), do_soft = (MODE != 2 && MODE != 3);
+  const bool do_mfma = (MODE != 4 && MODE != 5 && MODE != 7 && MODE != 9), do_soft = (MODE != 2 && MODE != 3 && MODE != 12);
   unsigned long long soft_cyc = 0;
   __syncthreads();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -83,7 +85,15 @@ __global__ __launch_bounds__(512, 1) void probe(unsigned long long* out, float* 
       if (((ph + g) & 1) == 0) {
         if (do_mfma) {
           __builtin_amdgcn_s_setprio(1);
-          if constexpr (MODE != 1 && MODE != 3) {
+          if constexpr (MODE == 11 || MODE == 12) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+              for (int t = 0; t < 2; ++t) {
+                c32[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[(k + t) & 3], fb[k], c32[t], 0, 0, 0);
+                c32[2 + t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[(k + t) & 3], fa[k], c32[2 + t], 0, 0, 0);
+              }
+          } else if constexpr (MODE != 1 && MODE != 3) {
             // Sᵀ: 2 chains x 4 k-steps; PV: 2 chains x 4 k-steps
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -176,7 +186,7 @@ void run(unsigned long long* out, float* sink, unsigned long long* host) {
   const double per = cyc / (blocks * 8) / (2.0 * iters);
   const double ghz = cyc / rt / 10.0;  // s_memrealtime: 100 MHz
   // matrix work: one tile (16 x 32x32x16 = 32 x 16x16x32) per SIMD per interval
-  const bool mf = !(MODE == 4 || MODE == 5 || MODE == 7 || MODE == 9);
+  const bool mf = !(MODE == 4 || MODE == 5 || MODE == 7 || MODE == 9);  // (11, 12: MFMAs)
   const double flops = mf ? 2.0 * 32 * 32 * 16 * 16 * 4 * blocks * 2.0 * iters : 0.0;
   // each wave runs the softmax in iters intervals (half of them)
   const double soft = sc / (blocks * 8) / iters;
@@ -202,6 +212,8 @@ int main() {
     run<8>(out, sink, host);
     run<9>(out, sink, host);
     run<10>(out, sink, host);
+    run<11>(out, sink, host);
+    run<12>(out, sink, host);
   }
   return 0;
 }

@@ -9,6 +9,9 @@
 //   mode 2: pinned, per MFMA: 1 MFMA, 2 transcendental, 2 VALU (the rest after the last MFMA)
 //   mode 3: MFMAs only (the matrix floor)
 //   mode 4: VALU only (the issue floor of the softmax alone)
+//   mode 5: the segment written as 8 chunks fenced by sched_barrier(0), each chunk 2 MFMAs (one Sᵀ,
+//           one PV) and one eighth of the softmax (4 exp2, 2 cvt_pk, 2 dot2c, one max step)
+//   mode 6: as 5 with 4 chunks of 4 MFMAs
 // One workgroup of 4 waves (one per SIMD) per CU, random operands.  Prints cycles per segment
 // (s_memtime), the in-kernel clock and the MFMA TF/s.  Build with -mllvm -amdgpu-mfma-vgpr-form=1
 // (accumulators in VGPRs: the softmax reads them without v_accvgpr_read copies).  Usage: sw_probe
@@ -51,6 +54,7 @@ __global__ __launch_bounds__(256, 1) void probe(unsigned long long* out, float* 
   float la[4] = {0.f, 0.f, 0.f, 0.f}, lb[4] = {0.f, 0.f, 0.f, 0.f};
   uint32_t pm = 0;
   constexpr bool MF = MODE != 4, SM = MODE != 3;
+  constexpr int NCH = MODE == 5 ? 8 : 4;  // (modes 5, 6) chunks per segment
 
   // one segment: Sᵀ of block X (sx) and PV of block X (ox, with px); softmax of block Y (sy -> py),
   // row sums of Y's previous P (ly)
@@ -100,6 +104,45 @@ __global__ __launch_bounds__(256, 1) void probe(unsigned long long* out, float* 
       }
     }
   };
+  // modes 5 / 6: chunk k of a segment carries Sᵀ k-step(s) and PV k-step(s) of block X and pairs
+  // 2k..2k+1 (mode 5) of block Y's softmax, fenced
+  auto segment_chunked = [&](floatx16 (&sx)[2], const half8 (&qx)[4], floatx16 (&ox)[2], uint32_t (&px)[4][4],
+                             const floatx16 (&sy)[2], uint32_t (&py)[4][4], float (&ly)[4]) __attribute__((always_inline)) {
+    const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
+    uint32_t pn[4][4];
+    half2v mx2[2] = {{(_Float16)0.f, (_Float16)0.f}, {(_Float16)0.f, (_Float16)0.f}};
+    constexpr int MPC = 16 / NCH;  // MFMAs per chunk
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+      for (int m = 0; m < MPC; ++m) {
+        const int idx = ch * MPC + m;  // 0..15: even Sᵀ, odd PV (k-step idx / 4, chain)
+        const int k = (idx >> 1) >> 1, t = (idx >> 1) & 1;
+        if ((idx & 1) == 0) {
+          sx[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[k][t], qx[k], k == 0 ? floatx16{} : sx[t], 0, 0, 0);
+        } else {
+          const half8 p = __builtin_bit_cast(half8, u32x4{px[k][0], px[k][1], px[k][2], px[k][3]});
+          ox[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[k][t], p, ox[t], 0, 0, 0);
+        }
+      }
+      // pairs (s, x) = 16 / NCH pairs of block Y
+#pragma unroll
+      for (int j = 0; j < 16 / NCH; ++j) {
+        const int pr = ch * (16 / NCH) + j, s_ = pr >> 2, x = pr & 3;
+        const float s0 = sy[s_ >> 1][8 * (s_ & 1) + 2 * x], s1 = sy[s_ >> 1][8 * (s_ & 1) + 2 * x + 1];
+        pn[s_][x] = __builtin_bit_cast(uint32_t, half2v{(_Float16)__builtin_amdgcn_exp2f(s0), (_Float16)__builtin_amdgcn_exp2f(s1)});
+        mx2[pr & 1] = __builtin_elementwise_maximum(mx2[pr & 1], __builtin_bit_cast(half2v, pn[s_][x]));
+        ly[x] = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2v, py[s_][x]), one2, ly[x], false);
+        asm volatile("" : "+v"(pn[s_][x]), "+v"(ly[x]), "+v"(mx2[pr & 1]));  // (pinned in its chunk)
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int s_ = 0; s_ < 4; ++s_)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) py[s_][x] = pn[s_][x];
+    pm ^= __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(mx2[0], mx2[1]));
+  };
   __syncthreads();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int it = 0; it < iters; ++it) {
@@ -107,10 +150,15 @@ __global__ __launch_bounds__(256, 1) void probe(unsigned long long* out, float* 
 #pragma unroll
       for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(sa[t]), "+v"(sb[t]));
     }
-    segment(sa, qa, oa, pa, sb, pb, lb);
-    __builtin_amdgcn_sched_barrier(0);
-    segment(sb, qb, ob, pb, sa, pa, la);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (MODE == 5 || MODE == 6) {
+      segment_chunked(sa, qa, oa, pa, sb, pb, lb);
+      segment_chunked(sb, qb, ob, pb, sa, pa, la);
+    } else {
+      segment(sa, qa, oa, pa, sb, pb, lb);
+      __builtin_amdgcn_sched_barrier(0);
+      segment(sb, qb, ob, pb, sa, pa, la);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   float acc = la[0] + la[1] + la[2] + la[3] + lb[0] + lb[1] + lb[2] + lb[3] + (float)pm;
@@ -159,6 +207,8 @@ int main() {
     run<2>(out, sink, host);
     run<3>(out, sink, host);
     run<4>(out, sink, host);
+    run<5>(out, sink, host);
+    run<6>(out, sink, host);
   }
   return 0;
 }
