@@ -125,7 +125,6 @@ __global__ __launch_bounds__(kThreads, (D >= 128 ? 1 : 2)) void bwd_f16_kernel(B
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
   using S = BSmem<D>;
-  constexpr float kNegInf = -__builtin_huge_valf();
 
   const int nq = a.rule.q.n, nk = a.rule.k.n, d = a.d, vd = a.v_d;
   const uint32_t nkb = (nk + kBK - 1) / kBK;

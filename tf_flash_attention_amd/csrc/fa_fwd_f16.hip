@@ -43,7 +43,6 @@ typedef __attribute__((address_space(3))) u32x2 lds_u32x2_t;
 
 constexpr int kBN = 64;      // keys per tile
 constexpr int kVPad = 2;     // V slab row padding, in 8-byte rows
-constexpr int kThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr float kRescaleThr = 8.f;  // log2 units (cdna_hip_programming.md T13)
@@ -57,7 +56,6 @@ __device__ __forceinline__ float xor32(float x) {
 // Structure flags (FA_FWD_VARIANT overrides the default for A/B timing runs)
 constexpr int kFOcc3 = 4;        // ask for 3 waves/SIMD (VGPR <= 168)
 constexpr int kFDot2 = 8;        // row sums of the fp16 P by v_dot2_f32_f16 (half the VALU ops)
-constexpr int kFHoistV = 2;      // read all V fragments before the PV MFMAs
 constexpr int kFOcc1 = 16;       // one wave per SIMD: the whole 512-entry register file
 constexpr int kFSched = 32;      // force a 1-MFMA/5-VALU interleave (sched_group_barrier)
 // row sums on the matrix pipe: one more MFMA per PV k-step with an all-ones A operand (every row of
@@ -514,7 +512,6 @@ hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s) {
     }
   }
   const bool pinned = v >= 0 && v < 1000;
-  if (v >= 2500 && v < 2600 && fwd_f16_trio_supported(a)) return launch_fwd_f16_trio(a, s);
 #else
   constexpr bool pinned = false;
 #endif

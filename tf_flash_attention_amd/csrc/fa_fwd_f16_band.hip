@@ -8,17 +8,19 @@
 // list of blocks ("items": the query blocks of consecutive (batch, head) slices in order)
 // as ONE stream of key tiles:
 //
-//   * every item is exactly T tile positions (T = the most tiles any block's band spans,
-//     rounded up to a multiple of 4, >= 12); positions past an item's band load zeros and are
-//     skipped by every wave.  The item loop is unrolled over its T positions, so ring slots,
-//     staging sets and every per-position decision are compile-time;
-//   * the K/V staging (registers, loads five / four positions ahead, stored two positions
-//     later; LDS rings of four slots) runs straight across item boundaries;
+//   * every item is exactly T positions (T + 2 a multiple of 4, 10 <= T <= 22); group 1 (queries
+//     128-255) works two key tiles ahead of group 0, so an item streams T + 2 tiles (a ws = 256
+//     band: 10 positions for 12 tiles).  Positions past an item's band load zeros and are skipped
+//     by every wave.  The item loop is unrolled over its T positions, so ring slots, staging
+//     registers and every per-position decision are compile-time;
+//   * the K/V staging (registers, loaded one position ahead of their LDS store, 1.2 tiles a
+//     position; LDS rings of four slots) runs straight across item boundaries;
 //   * the next item's Q image is loaded one 16-B chunk per thread at positions 2-5 and stored
 //     into the second of two LDS Q buffers one position later (3-6); each wave reads its new Q
 //     fragments in the VALU phase of the item's last position;
-//   * at position 0 of the next item the waves write the finished item's O (fp16, [c][256 q])
-//     over its dead Q buffer and its l / m beside it; at positions 2-3 whole 16-B rows leave
+//   * at positions 0-1 of the next item the waves write the finished item's O (fp16, [c][256 q])
+//     over its dead Q buffer and its l / m beside it (MFMA phases, beside the other group's
+//     softmax); at positions 2-3 whole 16-B rows leave
 //     for HBM (coalesced; the per-value stores of a per-block kernel touch 32-64 lines each);
 //   * every MFMA phase issues a fixed set of vector-memory operations, so hipcc's vmcnt waits
 //     stay exact (a conditional store anywhere in the stream made every staging store wait
@@ -31,13 +33,16 @@
 // Inside an item the structure is the ping-pong of fa_fwd_f16_pingpong.hip (eight waves, two
 // groups alternating MFMA and softmax phases, unconditional MFMAs with P zeroed for a wave's
 // skipped tiles, fp32 accumulation, log2-domain lazy rebase at 8, row sums in running
-// accumulators, l relative to the stored fp16 m).  Replaces the reference's ForwardImpl
+// accumulators, the rebase check on the packed P, l relative to the stored fp16 m).  Replaces the reference's ForwardImpl
 // (flash_attention.cu:425-1077) under LocalAttentionPolicy (flash_attention.h:117-140) for
 // these shapes.
+//
+// Structures measured against this one (the unstaggered item, the whole epilogue in VALU(0), staging
+// two positions ahead, LDS-DMA staging, packed edge-mask bounds, a hand-ordered softmax stream) and
+// the stamp / ablation builds were taken out in round 5; their numbers are in DESIGN.md §3.0c, §6.
 #include "fa_device.h"
 #include "fa_kernels.h"
 #include "fa_mfma.h"
-#include "fa_softmax_stream.h"
 
 #include <string.h>
 
@@ -60,63 +65,13 @@ constexpr int kOffLM = kOffV + kNS * kTile;   // l (fp32) and m (fp16) of a fini
 constexpr int kOffTab = kOffLM + 6 * kBM;     // kt0 of every query block of a slice (int32)
 constexpr int kMaxTab = 4096;                 // query blocks per slice: nq <= 1M
 constexpr int kSmem = kOffTab + 4 * kMaxTab;  // 145.5 KB
-// Item timeline (positions it = 0 .. T-1 of item n+1): VALU(0) writes item n's O / l / m into
-// LDS (O over Q buffer n&1, dead by then); MFMA(2), MFMA(3) store it to HBM; MFMA(2..5) load
-// item n+2's Q chunks, MFMA(3..6) store them into buffer n&1 (after the O reads); VALU(T-1)
-// reads them as fragments: with T >= 12 a barrier separates every store from every read.
-constexpr int kMinT = 12;
-// structure flags: the rebase check and m on the packed P (fa_fwd_f16_pingpong.hip's kFPMax; the
-// default since round 3; 0 = round 2's exact fp32 row max on every tile)
-constexpr int kBFPMax = 1;
-// timing ablations (diagnostic library only; outputs WRONG): no edge masks, no softmax (P = S
-// rounded), every staging load re-reading one hot tile (L2-resident), no staging LDS stores.  (An
-// ablation that drops the output — the O epilogue — lets hipcc delete the PV work with it, so the
-// item-boundary traffic has none.)
-constexpr int kBANoMask = 2, kBANoSoftmax = 8, kBANoLoad = 16, kBANoStore = 32;
-// one staging register set: the K / V loads run one position ahead of their store instead of two
-constexpr int kBLead1 = 64;
-// staggered groups: group 1 (queries 128-255 of the item) works on tile p + 2 where group 0 works on
-// tile p, so an item is T' positions for T' + 2 tiles instead of T positions for T tiles (a 256-query
-// item of a ws = 256 band: 10 positions instead of 12; each group's four waves span 10 tiles).  The
-// stream stages 1.2 tiles a position (two at the item boundary, see stag_k / stag_v), loads one
-// position ahead of their store.
-constexpr int kBStag = 128;
-constexpr int kMinTStag = 10;
-constexpr int kMaxTStag = 22;
-// the finished item's epilogue out of VALU(0): l / m and the new item's lane state at the tail of
-// MFMA(0); O into LDS there too for group 1, at the head of MFMA(1) for group 0 (each beside the
-// other group's first softmax, instead of stretching its own VALU(0))
-constexpr int kBEpiSplit = 256;
-// the exponentials of a P k-step (8) issued as one batch into their own registers before its four
-// conversions: at ~235 VGPRs hipcc reused two temporaries, so every v_cvt_pk_f16_f32 waited on the
-// v_exp_f32 just before it (an s_nop plus the transcendental latency, 16 times a tile)
-constexpr int kBExpBatch = 1024;
-// (staggered) the staging loads two positions ahead of their stores instead of one, in two register
-// sets (by position parity).  Measured within 0.5 % of one position: not taken
-constexpr int kBLead2 = 2048;
-// (staggered) the staging by LDS-DMA (inline-asm `buffer_load_dwordx4 ... lds`, no staging registers,
-// no ds_write_b128): each wave fetches its 8 channel rows of a group's tile chunk straight into the
-// ring slot at the point the register form stored it, the lanes' source chunks permuted so the
-// contiguous 1 KB the wave writes is the swizzled row image; every wave waits vmcnt(0) at the end of
-// the next VALU phase, before the barrier that publishes the slot (hipcc does not see these loads)
-constexpr int kBDma = 4096;
-// timing ablation of kBDma (outputs WRONG): no vmcnt wait before the publishing barrier
-constexpr int kBANoDmaWait = 8192;
-// the edge mask's bounds as fp32 pairs (v_pk_add_f32: each pair the previous plus 2 or 10 key steps,
-// exact: multiples of 2^99 below 2^113), 16 packed adds instead of 32 v_fmamk; bitwise unchanged,
-// 2-3 % slower on c4 (one dependent chain): diagnostic only
-constexpr int kBMaskPk = 16384;
-// (with kBMaskPk) the pairs as two independent chains of eight, one per 32-key half
-constexpr int kBMaskPk2 = 32768;
-// the exp2 / pack / packed-max part of a non-first tile's softmax as the hand-ordered stream of
-// fa_softmax_stream.h (the conversions one pair behind their exponentials)
-constexpr int kBAsmSm = 65536;
-constexpr int kBandR3Final = kBFPMax | kBStag | kBEpiSplit;  // round 3: staggered groups, split epilogue
-// round 4: + exponentials in batches (c4, one process: 4.109-4.147 against 4.139-4.194 ms; outputs
-// bitwise unchanged)
-constexpr int kBandDefault = kBandR3Final | kBExpBatch;
-constexpr int kBandR3 = kBFPMax;                             // round 3 before the stagger: T positions for T tiles
-
+// Item timeline (positions it = 0 .. T-1 of item n+1): MFMA(0) writes item n's l / m (and group
+// 1's O) into LDS, MFMA(1) group 0's O (O over Q buffer n&1, dead by then); MFMA(2), MFMA(3) store
+// it to HBM; MFMA(2..5) load item n+2's Q chunks, MFMA(3..6) store them into buffer n&1 (after the
+// O reads); VALU(T-1) reads them as fragments: with T >= 10 a barrier separates every store from
+// every read.
+constexpr int kMinT = 10;
+constexpr int kMaxT = 22;
 // staggered staging schedule (T positions, NT = T + 2 tiles an item, rings of four slots: tile j in
 // slot j & 3).  Tile j of an item is read by group 0 as K at position j (j < T) and as V at j + 1, by
 // group 1 as K at j - 2 and as V at j - 1 (j >= 2).  A group's chunk of a tile is stored in its MFMA
@@ -161,9 +116,9 @@ __device__ __forceinline__ void store_data_guard() {
   __builtin_amdgcn_sched_barrier(0);
 }
 // masked scores sit at or below -2^99 (the arithmetic edge mask); a row maximum at or below this
-// floor means "nothing allowed yet" (never a reference), and is the unset state of thr.  Every
-// finite score formed from fp16 inputs lies far inside (-2^98, 2^99), so no allowed score is clipped
-// and no disallowed one stays above an allowed one (the 2^20 scale had a +-2^18 range).
+// floor means "nothing allowed yet" (never a reference).  Every finite score formed from fp16 inputs
+// lies far inside (-2^98, 2^99), so no allowed score is clipped and no disallowed one stays above an
+// allowed one (the 2^20 scale had a +-2^18 range).
 constexpr float kMaskFloor = -0x1p98f;
 
 struct BandArgs {
@@ -190,23 +145,19 @@ struct Item {
   int32_t kt0;  // first key of its first tile (nk past the list: every load reads zeros)
 };
 
-// T (positions per item) is a template parameter, a multiple of 4: the item loop is unrolled over
-// its positions, so ring slots, staging sets and every "which position of the item" decision are
-// compile-time (no per-phase selects or dummy operations) and a position p = n*T + it has
-// p mod 4 == it mod 4
-template <int T, bool STAMP = false, int F = kBandDefault>
+// T (positions per item) is a template parameter, T + 2 a multiple of 4: the item loop is unrolled
+// over its positions, so ring slots, staging registers and every "which position of the item"
+// decision are compile-time (no per-phase selects or dummy operations)
+template <int T>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) {
-  constexpr bool PMAX = (F & kBFPMax) != 0;
-  constexpr bool STG = (F & kBStag) != 0;
-  constexpr int NT = STG ? T + 2 : T;  // tiles an item streams
+  constexpr int NT = T + 2;  // tiles an item streams
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
   const FwdArgs& a = ba.a;
   constexpr float kNegInf = -__builtin_huge_valf();
 
   const int nq = a.rule.q.n, nk = a.rule.k.n;
-  static_assert(STG ? ((T + 2) % 4 == 0 && T >= kMinTStag) : (T % 4 == 0 && T >= kMinT),
-                "T: a multiple of 4 (staggered: T + 2), at least kMinT (kMinTStag)");
+  static_assert((T + 2) % 4 == 0 && T >= kMinT && T <= kMaxT, "T: T + 2 a multiple of 4, in [kMinT, kMaxT]");
   const int nqb = (nq + kBM - 1) / kBM;
   // this workgroup's items: first + stride * local, inside [it_begin, it_end).
   //   contiguous: a run of consecutive items per workgroup (stride 1);
@@ -234,7 +185,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = w >> 2;  // waves w and w+4 share a SIMD
-  const int toff = STG ? 2 * grp : 0;  // staggered: this group's tile at position p is p + toff
+  const int toff = 2 * grp;  // this group's tile at position p is p + toff
   const int h = lane >> 5, r = lane & 31;
   const int gq = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const int d = a.d, vd = a.v_d;
@@ -253,17 +204,13 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   // into LDS, so the stream's item switch is a table read, not two binary searches
   const lds_char_t* tab = smem + kOffTab;
   for (int qb = threadIdx.x; qb < nqb; qb += kNW * 64) {
-    int kb, ke, kt;
-    if constexpr (STG) {  // the first tile group 0 needs, and two before group 1's first (may be < 0)
-      k_range_for_q_block(a.rule, qb * kBM, min(qb * kBM + kBM / 2, nq) - 1, &kb, &ke);
-      kt = ke > kb ? (kb / kBN) * kBN : nk;
-      if (qb * kBM + kBM / 2 < nq) {
-        k_range_for_q_block(a.rule, qb * kBM + kBM / 2, min(qb * kBM + kBM, nq) - 1, &kb, &ke);
-        if (ke > kb) kt = min(kt, (kb / kBN) * kBN - 2 * kBN);
-      }
-    } else {
-      k_range_for_q_block(a.rule, qb * kBM, min(qb * kBM + kBM, nq) - 1, &kb, &ke);
-      kt = (kb / kBN) * kBN;
+    // the first tile group 0 needs, and two before group 1's first (may be < 0)
+    int kb, ke;
+    k_range_for_q_block(a.rule, qb * kBM, min(qb * kBM + kBM / 2, nq) - 1, &kb, &ke);
+    int kt = ke > kb ? (kb / kBN) * kBN : nk;
+    if (qb * kBM + kBM / 2 < nq) {
+      k_range_for_q_block(a.rule, qb * kBM + kBM / 2, min(qb * kBM + kBM, nq) - 1, &kb, &ke);
+      if (ke > kb) kt = min(kt, (kb / kBN) * kBN - 2 * kBN);
     }
     *reinterpret_cast<__attribute__((address_space(3))) int*>(smem + kOffTab + 4 * qb) = kt;
   }
@@ -307,32 +254,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   const uint32_t kwo = crow * 128 + ((cm * 16) ^ ((crow & 2) << 5));
   const uint32_t vwo = crow * 128 + 16 * (cm ^ ((crow >> 1) & 7));
   auto load = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t slb, int k0) -> u32x4 __attribute__((always_inline)) {
-    if constexpr (STG) {  // (staggered items may start before key 0: those tiles read zeros)
-      const bool in = k0 >= 0 && k0 + 8 * cm < nk;
-      return __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off : 0x80000000u, slb + 2 * min(max(k0, 0), nk), 0);
-    }
-    const bool in = k0 + 8 * cm < nk;
-    return __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off : 0x80000000u, slb + 2 * min(k0, nk), 0);
+    // (an item may start before key 0: those tiles read zeros)
+    const bool in = k0 >= 0 && k0 + 8 * cm < nk;
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off : 0x80000000u, slb + 2 * min(max(k0, 0), nk), 0);
   };
   auto store = [&](int off, u32x4 v) __attribute__((always_inline)) { *reinterpret_cast<lds_u32x4_t*>(smem + off) = v; };
-  // (kBDma) lane L of wave w writes LDS bytes 1024 w + 16 L of the slot: channel row crow = tid >> 3,
-  // in-row chunk tid & 7, so it fetches the global chunk the swizzle puts there (kwo / vwo inverted)
-  auto dma = [&](__amdgpu_buffer_rsrc_t rs, bool isk, uint32_t slb, int k0, int lds_off) __attribute__((always_inline)) {
-    int t = tid;
-    asm volatile("" : "+v"(t));  // (recomputed where used: hoisted, the offsets would stay live)
-    const int rw = t >> 3;
-    const int cmx = isk ? ((t & 7) ^ ((rw & 2) << 1)) : ((t & 7) ^ ((rw >> 1) & 7));
-    const bool in = rw < (isk ? d : vd) && k0 >= 0 && k0 + 8 * cmx < nk;
-    const uint32_t off = in ? (uint32_t)rw * (uint32_t)nk * 2u + 16u * cmx : 0x80000000u;
-    const uint32_t m0v = (uint32_t)(uintptr_t)(smem + lds_off) + 1024u * (uint32_t)w;
-    const uint32_t so = __builtin_amdgcn_readfirstlane(slb + 2 * min(max(k0, 0), nk));
-    // (s_nop 0: the one wait state between the SALU write of M0 and an LDS-DMA that reads it)
-    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(off), "s"(rs), "s"(so), "{m0}"(m0v) : "memory");
-  };
   //      Q image [64][256] (64-B blocks XOR-swizzled by c&3): chunk j of a thread = channel row
   //      (tid>>5) + 16j, 8 queries at 8*(tid&31)
   const int qc0 = tid >> 5, qm = tid & 31;
-  const uint32_t qg_lane = (uint32_t)qc0 * (uint32_t)nq * 2u + 16u * qm;
   const uint32_t ql_lane = qc0 * kQRow + ((qm * 16) ^ ((qc0 & 3) << 6));
   // (inside the item loop the lane offsets are recomputed where used from an opaque copy of the
   // thread id: hoisted, they would stay live across the whole stream, a VGPR each)
@@ -349,12 +278,10 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
                                                  x.sl * qsl + 2 * min(x.q0, nq), 0);
   };
 
-  // ---- prologue: Q(item 0) into Q buffer 0, K(0..2) into ring slots 0..2, V(0..1) into slots
-  //      0..1 (slot 3 zeroed: the first PV reads "V(-1)" against P = 0), K(3..4) / V(2..3) into
-  //      the staging registers (positions 0..5 all belong to item 0: T >= 6)
-  constexpr bool LEAD2 = STG && (F & kBLead2) != 0;
+  // ---- prologue: Q(item 0) into Q buffer 0, K(0..2) and V(0) into their ring slots (V slots 1
+  //      and 3 zeroed: the first PV of each group reads them against P = 0); the chunks this
+  //      thread's group stores at position 0 into the staging registers
   u32x4 kst[2], vst[2];
-  u32x4 kst2[LEAD2 ? 2 : 1][2], vst2[LEAD2 ? 2 : 1][2];  // LEAD2: set p & 1 feeds the stores at position p
   {
     u32x4 kp[3], vp[2], qv[4];
 #pragma unroll
@@ -363,19 +290,8 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     for (int j = 0; j < 2; ++j) vp[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + j * kBN);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      if constexpr (LEAD2) {  // the chunks this thread's group stores at positions 0 and 1
-        kst2[0][j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 0, 1, j) : stag_k1(T, 0, 0, j)) * kBN);
-        vst2[0][j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 0, 1, j) : stag_v1(T, 0, 0, j)) * kBN);
-        kst2[1][j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 1, 1, j) : stag_k1(T, 1, 0, j)) * kBN);
-        vst2[1][j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 1, 1, j) : stag_v1(T, 1, 0, j)) * kBN);
-      } else if constexpr (STG && (F & kBDma) != 0) {  // (position 0's chunks fetched in MFMA(0))
-      } else if constexpr (STG) {  // the chunks this thread's group stores at position 0
-        kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 0, 1, j) : stag_k1(T, 0, 0, j)) * kBN);
-        vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 0, 1, j) : stag_v1(T, 0, 0, j)) * kBN);
-      } else {
-        kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (3 + j) * kBN);
-        vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (2 + j) * kBN);
-      }
+      kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 0, 1, j) : stag_k1(T, 0, 0, j)) * kBN);
+      vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 0, 1, j) : stag_v1(T, 0, 0, j)) * kBN);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) qv[j] = qload(cur, j);
@@ -383,15 +299,8 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     for (int j = 0; j < 4; ++j) store(ql_lane + j * 16 * kQRow, qv[j]);
 #pragma unroll
     for (int j = 0; j < 3; ++j) store(kOffK + j * kTile + kwo, kp[j]);
-    if constexpr (STG) {
-      // staggered: K(0..2) and V(0) are the tiles the schedule stores before position 0; V slots 1 and
-      // 3 feed the first PV of each group (P = 0) and are zeroed
-      store(kOffV + vwo, vp[0]);
-      store(kOffV + kTile + 16 * tid, u32x4{0, 0, 0, 0});
-    } else {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) store(kOffV + j * kTile + vwo, vp[j]);
-    }
+    store(kOffV + vwo, vp[0]);
+    store(kOffV + kTile + 16 * tid, u32x4{0, 0, 0, 0});
     store(kOffV + 3 * kTile + 16 * tid, u32x4{0, 0, 0, 0});
   }
   __syncthreads();
@@ -494,7 +403,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     o[1][i] = 0.f;
     negm[i] = 0.f;
   }
-  float m_run = 0.f, m_max = kNegInf, thr = kMaskFloor;
+  float m_run = 0.f, m_max = kNegInf;
   float lacc[4] = {0.f, 0.f, 0.f, 0.f};
 
   // edge-tile mask, arithmetic: key k0 + 8h + off is allowed iff 0 <= base + off < kspan (base = k0 +
@@ -516,32 +425,6 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     for (int pass = 0; pass < npass; ++pass) {
       const bool lo = (cls == 3) || (cls == 1 && pass == 0);
       const float cc = lo ? ca : cb, sg = lo ? kBig : -kBig;
-      if constexpr ((F & kBMaskPk) != 0) {
-        typedef float f2v __attribute__((ext_vector_type(2)));
-        const f2v d2 = {2.f * sg, 2.f * sg}, d10 = {10.f * sg, 10.f * sg};
-        if constexpr ((F & kBMaskPk2) != 0) {  // two independent chains (t = 0, 1), interleaved
-          f2v b[2] = {{cc, cc + sg}, {cc + 32.f * sg, cc + 33.f * sg}};
-#pragma unroll
-          for (int i = 0; i < 16; i += 2)
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-              if (i > 0) b[t] += (i & 7) == 0 ? d10 : d2;
-              st[t][i] = fminf(st[t][i], b[t].x);
-              st[t][i + 1] = fminf(st[t][i + 1], b[t].y);
-            }
-          continue;
-        }
-        f2v bnd = {cc, cc + sg};  // keys 0, 1 of the tile (relative to the lane's half)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int i = 0; i < 16; i += 2) {
-            if (t + i > 0) bnd += (i & 7) == 0 ? d10 : d2;  // key 32t + 16(i>>3) + (i&7)
-            st[t][i] = fminf(st[t][i], bnd.x);
-            st[t][i + 1] = fminf(st[t][i + 1], bnd.y);
-          }
-        continue;
-      }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -549,28 +432,20 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
           st[t][i] = fminf(st[t][i], __builtin_fmaf(sg, (float)(32 * t + 16 * (i >> 3) + (i & 7)), cc));
     }
   };
+  // the exponentials of a P k-step (8) issued as one batch into their own registers before its four
+  // conversions (at ~235 VGPRs hipcc otherwise reuses two temporaries, so every v_cvt_pk_f16_f32
+  // waits on the v_exp_f32 just before it: an s_nop plus the transcendental latency, 16 times a tile)
   auto exp_cvt = [&]() __attribute__((always_inline)) {
-    if constexpr ((F & kBExpBatch) != 0) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float e[8];
+    for (int s = 0; s < 4; ++s) {
+      float e[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) e[j] = __builtin_amdgcn_exp2f(st[s >> 1][8 * (s & 1) + j]);
-        asm volatile("" : "+v"(e[0]), "+v"(e[1]), "+v"(e[2]), "+v"(e[3]), "+v"(e[4]), "+v"(e[5]), "+v"(e[6]), "+v"(e[7]));
+      for (int j = 0; j < 8; ++j) e[j] = __builtin_amdgcn_exp2f(st[s >> 1][8 * (s & 1) + j]);
+      asm volatile("" : "+v"(e[0]), "+v"(e[1]), "+v"(e[2]), "+v"(e[3]), "+v"(e[4]), "+v"(e[5]), "+v"(e[6]), "+v"(e[7]));
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
-          pw[s][x] = __builtin_bit_cast(uint32_t, half2v{(_Float16)e[2 * x], (_Float16)e[2 * x + 1]});
-      }
-      return;
+      for (int x = 0; x < 4; ++x)
+        pw[s][x] = __builtin_bit_cast(uint32_t, half2v{(_Float16)e[2 * x], (_Float16)e[2 * x + 1]});
     }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const float s0 = st[s >> 1][8 * (s & 1) + 2 * x], s1 = st[s >> 1][8 * (s & 1) + 2 * x + 1];
-        pw[s][x] = __builtin_bit_cast(uint32_t, half2v{(_Float16)__builtin_amdgcn_exp2f(s0),
-                                                       (_Float16)__builtin_amdgcn_exp2f(s1)});
-      }
   };
   // the exact fp32 row max of the tile (both key halves)
   auto row_max = [&]() -> float __attribute__((always_inline)) {
@@ -584,7 +459,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         mx[j] = fmaxf(fmaxf(mx[j], st[j >> 1][8 * (j & 1) + i]), st[j >> 1][8 * (j & 1) + i + 1]);
     return max_pair32(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
   };
-  // PMAX: the running max of P over the current epoch (per lane) and 2^thr (-1: no reference yet)
+  // the running max of P over the current epoch (per lane) and 2^thr (-1: no reference yet)
   half2v pmr = {(_Float16)0.f, (_Float16)0.f};
   _Float16 thr_h = (_Float16)-1.f;
   auto pmax_tile = [&]() -> half2v __attribute__((always_inline)) {
@@ -600,18 +475,15 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     return M3(M3(a0, H(1, 3), H(3, 3)), b0, b0);
   };
   auto softmax = [&](int it, int cls, bool first) __attribute__((always_inline)) {
-    if (cls != 2 && !(F & kBANoMask)) mask(cur.kt0 + it * kBN, cls);
+    if (cls != 2) mask(cur.kt0 + it * kBN, cls);
     if (first) {  // an item's first tile: nothing to rescale (O and l start fresh): seed, then exp once
       const float mt = row_max();
       m_max = fmaxf(m_max, m_run + mt);
       const bool seed = mt > kMaskFloor;  // else (an empty row so far) a later tile seeds
       const float delta = seed ? mt : 0.f;
       m_run += delta;
-      if constexpr (!PMAX) thr = seed ? kRescaleThr : kMaskFloor;
-      if constexpr (PMAX) {
-        thr_h = seed ? (_Float16)(1 << (int)kRescaleThr) : (_Float16)-1.f;
-        pmr = half2v{(_Float16)0.f, (_Float16)0.f};
-      }
+      thr_h = seed ? (_Float16)(1 << (int)kRescaleThr) : (_Float16)-1.f;
+      pmr = half2v{(_Float16)0.f, (_Float16)0.f};
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         st[0][i] -= delta;
@@ -619,21 +491,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         negm[i] = -m_run;
       }
       exp_cvt();
-    } else if constexpr (PMAX) {
-      // the rebase check on the packed P (fa_fwd_f16_pingpong.hip, kFPMax): the exponentials run
-      // against m_run anyway; the exact fp32 max is formed only in the (rare) rebase branch
-      half2v tm;
-      if constexpr ((F & kBAsmSm) != 0) {
-        uint32_t pm;
-        softmax_stream_tile<1>(st, pw, pm);
-        tm = __builtin_bit_cast(half2v, pm);
-      } else {
-        exp_cvt();
+    } else {
+      // the rebase check on the packed P (as fa_fwd_f16_pingpong.hip): the exponentials run against
+      // m_run anyway; the exact fp32 max is formed only in the (rare) rebase branch
+      exp_cvt();
 #pragma unroll
-        for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
-          asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
-        tm = pmax_tile();
-      }
+      for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
+        asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
+      const half2v tm = pmax_tile();
       const _Float16 tmx = __builtin_elementwise_maximum(tm[0], tm[1]);
       const half2v pmr_old = pmr;
       pmr = __builtin_elementwise_maximum(pmr, tm);
@@ -642,7 +507,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         // close the epoch: its P maximum (approximate) and this tile (exact) into m_max
         const float pold = (float)__builtin_elementwise_maximum(pmr_old[0], pmr_old[1]);
         m_max = fmaxf(m_max, fmaxf(m_run + mt, m_run + __log2f(pold)));
-        // (PMAX: thr_h alone carries the state: -1 until the row has a reference)
+        // (thr_h alone carries the state: -1 until the row has a reference)
         const bool unset = thr_h < (_Float16)0.f;
         const bool seed = unset && (mt > kMaskFloor);
         const float delta = unset ? (seed ? mt : 0.f) : fmaxf(mt, 0.f);
@@ -662,32 +527,6 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         exp_cvt();
         pmr = half2v{(_Float16)0.f, (_Float16)0.f};
       }
-    } else {
-      const float mt = row_max();
-      m_max = fmaxf(m_max, m_run + mt);
-      exp_cvt();
-#pragma unroll
-      for (int x = 0; x < 4; ++x)  // pinned here: else they sink past the (rare) rebase branch
-        asm volatile("" : "+v"(pw[x][0]), "+v"(pw[x][1]), "+v"(pw[x][2]), "+v"(pw[x][3]));
-      if (__any(mt > thr)) {
-        const bool unset = thr < 0.f;
-        const bool seed = unset && (mt > thr);
-        const float delta = unset ? (seed ? mt : 0.f) : fmaxf(mt, 0.f);
-        const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
-        m_run += delta;
-        thr = (unset && !seed) ? thr : kRescaleThr;
-#pragma unroll
-        for (int x = 0; x < 4; ++x) lacc[x] *= alpha;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          o[0][i] *= alpha;
-          o[1][i] *= alpha;
-          st[0][i] -= delta;
-          st[1][i] -= delta;
-          negm[i] = -m_run;
-        }
-        exp_cvt();
-      }
     }
     const half2v one2 = {(_Float16)1.f, (_Float16)1.f};
 #pragma unroll
@@ -701,13 +540,12 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   int n = 0;  // local item index (positions of the item are static in the unrolled body)
 
   // O, l, m of the item that just finished (its last PV ran in the MFMA phase before) into LDS:
-  // O [c][256 q] fp16 over the finished item's Q buffer, l / m at the l/m area
-  // (kBEpiSplit) the parts: l / m into LDS (returns 1/l), O into LDS
+  // O [c][256 q] fp16 over the finished item's Q buffer, l / m at the l/m area; in two parts: l / m
+  // (returns 1/l), O
   auto epi_lm = [&]() -> float __attribute__((always_inline)) {
     const float l_tot = sum_pair32((lacc[0] + lacc[1]) + (lacc[2] + lacc[3]));
     const float inv = (l_tot > 0.f) ? __builtin_amdgcn_rcpf(l_tot) : 0.f;
-    const float m_fin = PMAX ? max_pair32(fmaxf(m_max, m_run + __log2f((float)__builtin_elementwise_maximum(pmr[0], pmr[1]))))
-                             : m_max;
+    const float m_fin = max_pair32(fmaxf(m_max, m_run + __log2f((float)__builtin_elementwise_maximum(pmr[0], pmr[1]))));
     if (h == 0) {
       float lv = 0.f;
       __half mv = neg_inf_approx<__half>();
@@ -732,49 +570,17 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
   };
-  float oinv = 0.f;  // (kBEpiSplit, group 0) the finished item's 1/l from MFMA(0) to MFMA(1)
+  float oinv = 0.f;  // (group 0) the finished item's 1/l from MFMA(0) to MFMA(1)
   auto item_switch = [&]() __attribute__((always_inline)) {
     const float inv = epi_lm();
     if (grp == 1) epi_o(inv);
     else oinv = inv;
     m_max = kNegInf;
-    if constexpr (!PMAX) thr = kMaskFloor;
-    m_run = 0.f;
-    if constexpr (PMAX) {
-      pmr = half2v{(_Float16)0.f, (_Float16)0.f};
-      thr_h = (_Float16)-1.f;
-    }
+    m_run = 0.f;  // (this item's first Sᵀ ran against -m = 0: see the end of VALU(T-1))
+    pmr = half2v{(_Float16)0.f, (_Float16)0.f};
+    thr_h = (_Float16)-1.f;
     item_state(cur);
   };
-  auto epilogue_lds = [&]() __attribute__((always_inline)) {
-    const float l_tot = sum_pair32((lacc[0] + lacc[1]) + (lacc[2] + lacc[3]));
-    const float inv = (l_tot > 0.f) ? __builtin_amdgcn_rcpf(l_tot) : 0.f;
-    // (PMAX: m_max is per lane; the open epoch's P maximum closes it)
-    const float m_fin = PMAX ? max_pair32(fmaxf(m_max, m_run + __log2f((float)__builtin_elementwise_maximum(pmr[0], pmr[1]))))
-                             : m_max;
-    lds_char_t* ob = smem + ((n + 1) & 1) * kQImg + 2 * (32 * w + r);
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int cch = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-        *reinterpret_cast<__attribute__((address_space(3))) _Float16*>(ob + cch * kQRow) = (_Float16)(o[u][i] * inv);
-        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // a few values at a time (register peak)
-      }
-    if (h == 0) {
-      float lv = 0.f;
-      __half mv = neg_inf_approx<__half>();
-      if (l_tot > 0.f) {
-        mv = __float2half(m_fin * kLn2);
-        // l relative to the STORED (rounded) m, so exp(s - m)/l is exact downstream
-        lv = l_tot * __builtin_amdgcn_exp2f(m_run - __half2float(mv) * kLog2e);
-      }
-      *reinterpret_cast<__attribute__((address_space(3))) float*>(smem + kOffLM + 4 * (32 * w + r)) = lv;
-      *reinterpret_cast<__attribute__((address_space(3))) unsigned short*>(smem + kOffLM + 4 * kBM + 2 * (32 * w + r)) =
-          __half_as_ushort(mv);
-    }
-  };
-
   // the next item's Q chunk in flight (loaded at positions 2-5, stored one position later: one
   // set of registers; the load has a whole position to land)
   u32x4 qst;
@@ -791,18 +597,17 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   // at 2-3 and into LDS at 4-5)
   auto mfma_phase = [&](auto IT_) __attribute__((always_inline)) {
     constexpr int it = decltype(IT_)::value;
-    constexpr bool L1 = (F & kBLead1) != 0;
-    constexpr int c = it & 3, x = L1 ? 0 : it & 1, kA = L1 ? 4 : 5;  // kA: the K tile loaded, positions ahead
+    constexpr int c = it & 3;
     __builtin_amdgcn_s_setprio(1);
-    // (staggered: this group's tiles are p + toff, toff in {0, 2}, tile j in slot j & 3, and
-    // (j + toff) & 3 = (j & 3) ^ toff; the PV at position 0 is of the previous item's tile T-1+toff)
-    constexpr int cv = (STG && it == 0) ? ((T - 1) & 3) : ((c + 3) & 3);
-    const lds_char_t* pk = smem + kOffK + (STG ? (c ^ toff) : c) * kTile;
-    const lds_char_t* pv = smem + kOffV + (STG ? (cv ^ toff) : cv) * kTile;
+    // (this group's tiles are p + toff, toff in {0, 2}, tile j in slot j & 3, and (j + toff) & 3 =
+    // ((j & 3) + toff) & 3; the PV at position 0 is of the previous item's tile T-1+toff)
+    constexpr int cv = (it == 0) ? ((T - 1) & 3) : ((c + 3) & 3);
+    const lds_char_t* pk = smem + kOffK + (c ^ toff) * kTile;
+    const lds_char_t* pv = smem + kOffV + (cv ^ toff) * kTile;
     // every fragment is read in the phase that uses it, two k-steps ahead (nothing lives across
     // the VALU phase: the register budget holds the stream's staging); the first two K k-steps
     // are read at the phase start, their latency the only one exposed
-    if constexpr ((F & kBEpiSplit) != 0 && it == 1) {  // group 0: the finished item's O, before o restarts
+    if constexpr (it == 1) {  // group 0: the finished item's O, before o restarts
       if (grp == 0 && n > 0) {
         epi_o(oinv);
         __builtin_amdgcn_sched_barrier(0);
@@ -842,23 +647,17 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // PV k-steps 2-3
     // staging: K(+3), V(+2) into the ring; loads of K(+5), V(+4) (this item's or the next's)
-    if constexpr (STG) {  // the group's tiles of this position (stag_k1 / stag_v1), tile j in slot j & 3
-      if constexpr (!(F & kBANoStore) && !(F & kBDma)) {
-        static_for<0, stag_nk(T, it)>([&](auto I_) __attribute__((always_inline)) {
-          constexpr int i = decltype(I_)::value, j0 = stag_k1(T, it, 0, i), j1 = stag_k1(T, it, 1, i);
-          const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
-          store(kOffK + (j & 3) * kTile + kwo, LEAD2 ? kst2[(it & 1) % (LEAD2 ? 2 : 1)][i] : kst[i]);
-        });
-        static_for<0, stag_nv(T, it)>([&](auto I_) __attribute__((always_inline)) {
-          constexpr int i = decltype(I_)::value, j0 = stag_v1(T, it, 0, i), j1 = stag_v1(T, it, 1, i);
-          const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
-          store(kOffV + (j & 3) * kTile + vwo, LEAD2 ? vst2[(it & 1) % (LEAD2 ? 2 : 1)][i] : vst[i]);
-        });
-      }
-    } else if constexpr (!(F & kBANoStore)) {
-      store(kOffK + ((c + 3) & 3) * kTile + kwo, kst[x]);
-      store(kOffV + ((c + 2) & 3) * kTile + vwo, vst[x]);
-    }
+    // (the group's tiles of this position: stag_k1 / stag_v1, tile j in slot j & 3)
+    static_for<0, stag_nk(T, it)>([&](auto I_) __attribute__((always_inline)) {
+      constexpr int i = decltype(I_)::value, j0 = stag_k1(T, it, 0, i), j1 = stag_k1(T, it, 1, i);
+      const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
+      store(kOffK + (j & 3) * kTile + kwo, kst[i]);
+    });
+    static_for<0, stag_nv(T, it)>([&](auto I_) __attribute__((always_inline)) {
+      constexpr int i = decltype(I_)::value, j0 = stag_v1(T, it, 0, i), j1 = stag_v1(T, it, 1, i);
+      const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
+      store(kOffV + (j & 3) * kTile + vwo, vst[i]);
+    });
     if constexpr (it >= 3 && it <= 6) {
       // the next item's Q chunk j = it-3 (channel rows 16j..16j+15) over the finished item's O,
       // whose rows 16j.. both groups read out at MFMA(2 + j/2), an interval or more before
@@ -897,52 +696,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       }
     }
     if constexpr (it >= 2 && it <= 5) qst = qload(nxt, it - 2);
-    if constexpr (STG && (F & kBANoLoad) != 0) {
-      // timing ablation (outputs WRONG): no staging loads, the stores write stale registers
-    } else if constexpr (STG && (F & kBDma) != 0) {
-      // this position's chunks straight into their ring slots (where the register form stores them;
-      // the slots' previous tiles are dead here); tile j of the current item, or j - NT of the next
-      auto src = [&](int j0, int j1, uint32_t slsz, int& slb, int& k0) __attribute__((always_inline)) {
-        const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
-        const bool nx = j >= NT;
-        slb = (nx ? nxt.sl : cur.sl) * (int)slsz;
-        k0 = (nx ? nxt.kt0 : cur.kt0) + (nx ? j - NT : j) * kBN;
-      };
-      static_for<0, stag_nk(T, it)>([&](auto I_) __attribute__((always_inline)) {
-        constexpr int i = decltype(I_)::value, j0 = stag_k1(T, it, 0, i), j1 = stag_k1(T, it, 1, i);
-        int slb, k0;
-        src(j0, j1, ksl, slb, k0);
-        dma(krs, true, (uint32_t)slb, k0, kOffK + ((((j0 == j1) ? j0 : (grp ? j1 : j0))) & 3) * kTile);
-      });
-      static_for<0, stag_nv(T, it)>([&](auto I_) __attribute__((always_inline)) {
-        constexpr int i = decltype(I_)::value, j0 = stag_v1(T, it, 0, i), j1 = stag_v1(T, it, 1, i);
-        int slb, k0;
-        src(j0, j1, vsl, slb, k0);
-        dma(vrs, false, (uint32_t)slb, k0, kOffV + ((((j0 == j1) ? j0 : (grp ? j1 : j0))) & 3) * kTile);
-      });
-    } else if constexpr (LEAD2) {
-      // the chunks the group stores two positions on (the next item's positions 0 / 1 at T-2 / T-1),
-      // into the set those stores read; tile j of the current item, or j - NT of the next
-      constexpr int pn = it + 2 < T ? it + 2 : it + 2 - T, add = it + 2 < T ? 0 : NT, set = (it & 1) % (LEAD2 ? 2 : 1);
-      auto src = [&](int j0, int j1, uint32_t slsz, int& slb, int& k0) __attribute__((always_inline)) {
-        const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
-        const bool nx = j >= NT;
-        slb = (nx ? nxt.sl : cur.sl) * (int)slsz;
-        k0 = (nx ? nxt.kt0 : cur.kt0) + (nx ? j - NT : j) * kBN;
-      };
-      static_for<0, stag_nk(T, pn)>([&](auto I_) __attribute__((always_inline)) {
-        constexpr int i = decltype(I_)::value;
-        int slb, k0;
-        src(stag_k1(T, pn, 0, i) + add, stag_k1(T, pn, 1, i) + add, ksl, slb, k0);
-        kst2[set][i] = load(krs, koff, (uint32_t)slb, k0);
-      });
-      static_for<0, stag_nv(T, pn)>([&](auto I_) __attribute__((always_inline)) {
-        constexpr int i = decltype(I_)::value;
-        int slb, k0;
-        src(stag_v1(T, pn, 0, i) + add, stag_v1(T, pn, 1, i) + add, vsl, slb, k0);
-        vst2[set][i] = load(vrs, voff, (uint32_t)slb, k0);
-      });
-    } else if constexpr (STG) {
+    {
       // the chunks the group stores at the next position (the next item's position 0 at T-1), one
       // position ahead; tile j of the current item, or j - NT of the next
       constexpr int pn = it + 1 < T ? it + 1 : 0, add = it + 1 < T ? 0 : NT;
@@ -964,16 +718,8 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         src(stag_v1(T, pn, 0, i) + add, stag_v1(T, pn, 1, i) + add, vsl, slb, k0);
         vst[i] = load(vrs, voff, (uint32_t)slb, k0);
       });
-    } else if constexpr ((F & kBANoLoad) != 0) {  // timing ablation: every load re-reads tile 0 of slice 0
-      kst[x] = load(krs, koff, 0, 0);
-      vst[x] = load(vrs, voff, 0, 0);
-    } else {
-      if constexpr (it + kA < T) kst[x] = load(krs, koff, cur.sl * ksl, cur.kt0 + (it + kA) * kBN);
-      else kst[x] = load(krs, koff, nxt.sl * ksl, nxt.kt0 + (it + kA - T) * kBN);
-      if constexpr (it + kA - 1 < T) vst[x] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (it + kA - 1) * kBN);
-      else vst[x] = load(vrs, voff, nxt.sl * vsl, nxt.kt0 + (it + kA - 1 - T) * kBN);
     }
-    if constexpr ((F & kBEpiSplit) != 0 && it == 0) {
+    if constexpr (it == 0) {
       // the finished item's l / m (and group 1's O: its last PV ran above); the new item's state
       if (n > 0) {
         __builtin_amdgcn_sched_barrier(0);
@@ -988,29 +734,8 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   auto valu_phase = [&](auto IT_) __attribute__((always_inline)) {
     constexpr int it = decltype(IT_)::value;
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's staging stores / reads landed
-    if constexpr (it == 0 && (F & kBEpiSplit) == 0) {
-      if (n > 0) {
-        epilogue_lds();
-        __builtin_amdgcn_sched_barrier(0);  // the epilogue's temporaries die before the softmax's
-        m_max = kNegInf;
-        if constexpr (!PMAX) thr = kMaskFloor;  // the item's first allowed key seeds m_run (scores are relative to it)
-        m_run = 0.f;         // (this item's first Sᵀ ran against -m = 0: see the end of VALU(T-1))
-        if constexpr (PMAX) {
-          pmr = half2v{(_Float16)0.f, (_Float16)0.f};
-          thr_h = (_Float16)-1.f;
-        }
-        item_state(cur);
-      }
-    }
     const int cls = tcls(it + toff);
-    if (cls != 0 && (F & kBANoSoftmax)) {  // timing ablation: P = S rounded, nothing else
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-#pragma unroll
-        for (int z = 0; z < 4; ++z)
-          pw[y][z] = __builtin_bit_cast(uint32_t, half2v{(_Float16)st[y >> 1][8 * (y & 1) + 2 * z],
-                                                         (_Float16)st[y >> 1][8 * (y & 1) + 2 * z + 1]});
-    } else if (cls != 0) {
+    if (cls != 0) {
       softmax(it + toff, cls, it == 0);
     } else {  // the next (unconditional) PV must add nothing
 #pragma unroll
@@ -1030,24 +755,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
 #pragma unroll
       for (int i = 0; i < 16; ++i) negm[i] = 0.f;
     }
-    // (kBDma) this wave's chunks fetched in the MFMA phase before have landed: the barrier after this
-    // phase publishes them, two intervals after their issue, as the register form's stores
-    if constexpr (STG && (F & kBDma) != 0 && (F & kBANoDmaWait) == 0) __builtin_amdgcn_s_waitcnt(0x0F70);
   };
 
   if (grp == 1) __builtin_amdgcn_s_barrier();
-  // diagnostic build only (STAMP): s_memtime of waves 0 and 4 of workgroup 0 at the four phase
-  // edges of every position of its first four items, written over the last slice's Q (WRONG)
-  auto stamp = [&](int it, int k) __attribute__((always_inline)) {
-    if constexpr (STAMP) {
-      if (blockIdx.x == 0 && (w == 0 || w == 4) && lane == 0 && n < 4) {
-        const uint64_t t = __builtin_amdgcn_s_memtime();
-        // (into the LAST slice's Q: no store of this workgroup lands there)
-        uint64_t* dbg = reinterpret_cast<uint64_t*>(const_cast<void*>(a.Q)) + (a.b - 1) * (int64_t)d * nq / 4;
-        dbg[((n * T + it) * 4 + k) * 2 + (w >> 2)] = t;
-      }
-    }
-  };
   auto step = [&](auto IT_) __attribute__((always_inline)) {
     constexpr int it = decltype(IT_)::value;
     if constexpr (it == 0) {
@@ -1059,13 +769,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       }
     }
     __builtin_amdgcn_s_barrier();
-    stamp(it, 0);
     mfma_phase(IT_);
-    stamp(it, 1);
     __builtin_amdgcn_s_barrier();
-    stamp(it, 2);
     valu_phase(IT_);
-    stamp(it, 3);
   };
   // one extra (phantom) item at the end: its positions 0-3 carry the last item's PV, its O / l /
   // m into LDS and out to HBM; the rest only move zeros
@@ -1086,31 +792,12 @@ struct TCache {
   int T;
   bool valid;
 };
-thread_local TCache g_tcache = {{}, 0, false}, g_scache = {{}, 0, false};
+thread_local TCache g_scache = {{}, 0, false};
 
 }  // namespace
 
-int band_tiles_per_item(const FwdArgs& a) {
-  if (g_tcache.valid && !memcmp(&g_tcache.r, &a.rule, sizeof(Rule))) return g_tcache.T;
-  const int nq = a.rule.q.n;
-  const int nqb = (nq + kBM - 1) / kBM;
-  int T = 0;
-  for (int qb = 0; qb < nqb; ++qb) {  // host: exact per block (two binary searches each)
-    int kb, ke;
-    const int q0 = qb * kBM;
-    k_range_for_q_block(a.rule, q0, min(q0 + kBM, nq) - 1, &kb, &ke);
-    if (ke > kb) T = max(T, (ke - (kb / kBN) * kBN + kBN - 1) / kBN);
-  }
-  T = (max(T, kMinT) + 3) / 4 * 4;  // a multiple of 4: ring slots are static per position
-  g_tcache.r = a.rule;
-  g_tcache.T = T;
-  g_tcache.valid = true;
-  return T;
-}
-
-// staggered items (kBStag): positions T' an item takes when group 1 runs two tiles ahead of group 0
-// (the first tile two before group 1's first allowed key or at group 0's, whichever is lower); T' + 2
-// a multiple of 4, at least kMinTStag
+// positions T an item takes when group 1 runs two tiles ahead of group 0 (the first tile two before
+// group 1's first allowed key or at group 0's, whichever is lower); T + 2 a multiple of 4, >= kMinT
 int band_positions_stag(const FwdArgs& a) {
   if (g_scache.valid && !memcmp(&g_scache.r, &a.rule, sizeof(Rule))) return g_scache.T;
   const int nq = a.rule.q.n, nk = a.rule.k.n;
@@ -1127,7 +814,7 @@ int band_positions_stag(const FwdArgs& a) {
     if (ke0 > kb0) T = max(T, (ke0 - kt + kBN - 1) / kBN);
     if (g1 && ke1 > kb1) T = max(T, (ke1 - kt + kBN - 1) / kBN - 2);
   }
-  T = (max(T, kMinTStag) + 2 + 3) / 4 * 4 - 2;
+  T = (max(T, kMinT) + 2 + 3) / 4 * 4 - 2;
   g_scache.r = a.rule;
   g_scache.T = T;
   g_scache.valid = true;
@@ -1147,7 +834,7 @@ bool fwd_f16_band_supported(const FwdArgs& a) {
       (reinterpret_cast<uintptr_t>(a.Q) % 16) || nq % 8)
     return false;
   // a band: every block spans few tiles (else the per-launch kernels cover it at no loss)
-  if (band_positions_stag(a) > kMaxTStag) return false;
+  if (band_positions_stag(a) > kMaxT) return false;
   // the per-slice table of first key tiles lives in LDS: kMaxTab query blocks (nq <= 1M)
   if ((nq + kBM - 1) / kBM > kMaxTab) return false;
   // one descriptor per tensor spans a workgroup's slices: below 2^31 bytes
@@ -1159,11 +846,11 @@ bool fwd_f16_band_supported(const FwdArgs& a) {
   return span * 2 * (int64_t)dm * (nq > nk ? nq : nk) < (1ll << 31);
 }
 
-template <int T, bool STAMP = false, int F = kBandDefault>
+template <int T>
 hipError_t launch_band_t(const BandArgs& ba, hipStream_t s) {
-  hipError_t e = set_smem_once(reinterpret_cast<const void*>(fwd_f16_band_kernel<T, STAMP, F>), kSmem);
+  hipError_t e = set_smem_once(reinterpret_cast<const void*>(fwd_f16_band_kernel<T>), kSmem);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((fwd_f16_band_kernel<T, STAMP, F>), dim3((unsigned)ba.n_wg), dim3(kNW * 64), kSmem, s, ba);
+  hipLaunchKernelGGL((fwd_f16_band_kernel<T>), dim3((unsigned)ba.n_wg), dim3(kNW * 64), kSmem, s, ba);
   return hipGetLastError();
 }
 
@@ -1176,46 +863,9 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   ba.n_xcd = device_xcds();
   ba.inter = band_interleaved(ba.n_items, ba.n_wg, ba.n_xcd) ? 1 : 0;
 #ifdef FA_DIAG
-  // FA_FWD_VARIANT: 2400 the unstaggered structure (T positions for T tiles), 2401 its stamp build,
-  // 2402 either with the contiguous item order, 2403-2410 its ablations / A-B (T = 12 only), 2421
-  // the default's stamp build (T' = 10), 2422 the staggered kernel with the whole epilogue in VALU(0)
-  const int dv = diag_variant("FA_FWD_VARIANT");
-  if (dv == 2402) ba.inter = 0;  // round-2 order: contiguous runs of items
-  if (dv >= 2400 && dv < 2420 && dv != 2402) {
-    ba.T = band_tiles_per_item(a);
-    if (ba.T == 12) {
-      switch (dv) {
-        case 2401: return launch_band_t<12, true, kBandR3>(ba, s);
-        case 2403: return launch_band_t<12, false, 0>(ba, s);  // round-2 softmax (exact max)
-        case 2404: return launch_band_t<12, false, kBandR3 | kBANoMask>(ba, s);
-        case 2406: return launch_band_t<12, false, kBandR3 | kBANoSoftmax>(ba, s);
-        case 2408: return launch_band_t<12, false, kBandR3 | kBANoLoad>(ba, s);
-        case 2409: return launch_band_t<12, false, kBandR3 | kBANoStore>(ba, s);
-        case 2410: return launch_band_t<12, false, kBandR3 | kBLead1>(ba, s);
-        default: break;
-      }
-    }
-    switch (ba.T) {
-      case 12: return launch_band_t<12, false, kBandR3>(ba, s);
-      case 16: return launch_band_t<16, false, kBandR3>(ba, s);
-      case 20: return launch_band_t<20, false, kBandR3>(ba, s);
-      default: return launch_band_t<24, false, kBandR3>(ba, s);
-    }
-  }
-  if (dv == 2421 && ba.T == 10) return launch_band_t<10, true>(ba, s);
-  if (dv == 2422 && ba.T == 10) return launch_band_t<10, false, kBFPMax | kBStag | kBExpBatch>(ba, s);  // epilogue in VALU(0)
-  if (dv == 2424 && ba.T == 10) return launch_band_t<10, false, kBandR3Final>(ba, s);  // round-3 default
-  // timing ablations of the default (outputs WRONG): no edge masks, no softmax, no staging stores
-  if (dv == 2425 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoMask>(ba, s);
-  if (dv == 2426 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoSoftmax>(ba, s);
-  if (dv == 2427 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoStore>(ba, s);
-  if (dv == 2428 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBANoLoad>(ba, s);
-  if (dv == 2429 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBLead2>(ba, s);
-  if (dv == 2430 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBDma>(ba, s);
-  if (dv == 2431 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBDma | kBANoDmaWait>(ba, s);
-  if (dv == 2432 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBMaskPk>(ba, s);
-  if (dv == 2433 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBMaskPk | kBMaskPk2>(ba, s);
-  if (dv == 2440 && ba.T == 10) return launch_band_t<10, false, kBandDefault | kBAsmSm>(ba, s);
+  // FA_FWD_VARIANT=2402: the round-2 item order (contiguous runs of items per workgroup), for the
+  // L2-traffic comparison of DESIGN.md §3.0c
+  if (diag_variant("FA_FWD_VARIANT") == 2402) ba.inter = 0;
 #endif
   switch (ba.T) {
     case 10: return launch_band_t<10>(ba, s);

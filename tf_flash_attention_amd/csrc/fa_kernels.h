@@ -61,12 +61,6 @@ hipError_t launch_fwd_f16_pp(const FwdArgs& a, hipStream_t s);
 // ping-pong fp16 forward (8 waves, two groups alternating MFMA / softmax phases) — fa_fwd_f16_pingpong.hip
 bool fwd_f16_pingpong_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s);
-#ifdef FA_DIAG
-// three-group rotation fp16 forward (12 waves: one MFMA phase beside two softmax halves per SIMD,
-// full policy, max(d, v_d) <= 64) — diag/fa_fwd_f16_trio.hip, diagnostic library only
-bool fwd_f16_trio_supported(const FwdArgs& a);
-hipError_t launch_fwd_f16_trio(const FwdArgs& a, hipStream_t s);
-#endif
 // ping-pong fp16 forward for 64 < max(d, v_d) <= 128 — fa_fwd_f16_pingpong128.hip
 bool fwd_f16_pingpong128_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_pingpong128(const FwdArgs& a, hipStream_t s);
@@ -75,7 +69,6 @@ bool fwd_f16_wide_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_wide(const FwdArgs& a, hipStream_t s);
 // persistent band forward for 1d unit-stride local windows, 32 < max(d, v_d) <= 64 — fa_fwd_f16_band.hip
 bool fwd_f16_band_supported(const FwdArgs& a);
-int band_tiles_per_item(const FwdArgs& a);
 hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s);
 bool bwd_f16_supported(const BwdArgs& a);
 // fp32 MFMA forward — fa_fwd_f32.hip

@@ -55,55 +55,3 @@ if __name__ == "__main__":
     print(f"// lag {lag}, dlag {dlag}: {len(ins)} instructions, {nt} temporaries")
     print('"' + "\\n\\t".join(ins) + '"')
 
-
-def write_csrc_header(path):
-    """The product header (tf_flash_attention_amd/csrc/fa_softmax_stream.h): the no-sum streams and
-    a helper that runs one over a wave-tile's Sᵀ registers (fa_fwd_f16_pingpong.hip layout)."""
-    lines = ["// fa_softmax_stream.h — generated by tools/gen/softmax_stream.py (do not edit).",
-             "// The exp2 / fp16-pack / packed-max part of one 32-query x 64-key wave-tile's softmax as a",
-             "// hand-ordered instruction stream: every v_cvt_pk_f16_f32 reads exponentials issued at least LAG",
-             "// pairs earlier and every v_pk_maximum3_f16 packed dwords converted a pair earlier, so one wave",
-             "// issues it without waiting on the transcendental unit's latency (hipcc batches the",
-             "// exponentials and then waits on each conversion).  Device code only (gfx950).",
-             "#ifndef TF_FLASH_ATTENTION_AMD_FA_SOFTMAX_STREAM_H_",
-             "#define TF_FLASH_ATTENTION_AMD_FA_SOFTMAX_STREAM_H_",
-             "",
-             "#include \"fa_mfma.h\"",
-             "",
-             "namespace fa {",
-             "namespace mf {",
-             ""]
-    for lag in (1, 2):
-        ins, nt = stream(lag, 1, False)
-        lines.append(f"// lag {lag}: {len(ins)} instructions, {nt} temporaries")
-        lines.append(f"#define FA_SOFTMAX_STREAM_L{lag} \\")
-        lines.append('  "' + "\\n\\t".join(ins) + '"')
-        lines.append("")
-    lines += [
-        "// pw[s][x] = fp16 pair (exp2(st[s>>1][8(s&1)+2x]), exp2(st[s>>1][8(s&1)+2x+1])), pm = packed max of all",
-        "template <int LAG>",
-        "__device__ __forceinline__ void softmax_stream_tile(const floatx16 (&st)[2], uint32_t (&pw)[4][4], uint32_t& pm) {",
-        "  float t[6];",
-        "#define FA_SS_P(s) \"=&v\"(pw[s][0]), \"=&v\"(pw[s][1]), \"=&v\"(pw[s][2]), \"=&v\"(pw[s][3])",
-        "#define FA_SS_S(t) \"v\"(st[t][0]), \"v\"(st[t][1]), \"v\"(st[t][2]), \"v\"(st[t][3]), \"v\"(st[t][4]), \"v\"(st[t][5]), \\",
-        "    \"v\"(st[t][6]), \"v\"(st[t][7]), \"v\"(st[t][8]), \"v\"(st[t][9]), \"v\"(st[t][10]), \"v\"(st[t][11]), \"v\"(st[t][12]), \\",
-        "    \"v\"(st[t][13]), \"v\"(st[t][14]), \"v\"(st[t][15])",
-        "  if constexpr (LAG == 1)",
-        "    asm volatile(FA_SOFTMAX_STREAM_L1",
-        "                 : FA_SS_P(0), FA_SS_P(1), FA_SS_P(2), FA_SS_P(3), \"=&v\"(pm), \"=&v\"(t[0]), \"=&v\"(t[1]), \"=&v\"(t[2]), \"=&v\"(t[3])",
-        "                 : FA_SS_S(0), FA_SS_S(1));",
-        "  else",
-        "    asm volatile(FA_SOFTMAX_STREAM_L2",
-        "                 : FA_SS_P(0), FA_SS_P(1), FA_SS_P(2), FA_SS_P(3), \"=&v\"(pm), \"=&v\"(t[0]), \"=&v\"(t[1]), \"=&v\"(t[2]), \"=&v\"(t[3]),",
-        "                   \"=&v\"(t[4]), \"=&v\"(t[5])",
-        "                 : FA_SS_S(0), FA_SS_S(1));",
-        "#undef FA_SS_P",
-        "#undef FA_SS_S",
-        "}",
-        "",
-        "}  // namespace mf",
-        "}  // namespace fa",
-        "",
-        "#endif  // TF_FLASH_ATTENTION_AMD_FA_SOFTMAX_STREAM_H_",
-        ""]
-    open(path, "w").write("\n".join(lines))
