@@ -379,8 +379,8 @@ def test_odd_channels(d, vd):
 @pytest.mark.parametrize("d,vd", [(160, 160), (256, 256), (130, 300), (520, 72), (300, 1030)])
 @pytest.mark.parametrize("policy,ws,causal", [("full", 1, False), ("causal", 1, False), ("local", 40, True)])
 def test_wide_channels(dtype, d, vd, policy, ws, causal):
-    """Channel counts past the MFMA kernels' 128: the resident generic kernels up to 256 (fp16 /
-    fp32) / 128 (fp64) channels, the channel-chunked kernels past that (the reference has no fixed
+    """Channel counts past 128: the MFMA kernels up to 256 channels (fp16 for aligned tensors, fp32 and
+    fp64 always), the resident / channel-chunked generic kernels past that (the reference has no fixed
     channel cap either: its key tile is sized from shared memory, flash_attention.cu:1977-2067)."""
     run_case(dtype, policy, 1, "scale_front", (2,), d, vd, (97,), (150,), ws=ws, causal=causal, seed=d + vd)
 
@@ -427,6 +427,21 @@ def test_wide_channels_mfma_forward_f32(d, vd, policy, seq, mode, qs, ks, ws, ls
 ])
 def test_wide_channels_mfma_backward_f32(d, vd, policy, seq, mode, qs, ks, ws, ls, causal):
     run_case(np.float32, policy, seq, mode, (2,), d, vd, qs, ks, ws=ws, ls=ls, causal=causal, seed=d + 11 * vd)
+
+
+# fp64 forward + backward for 128 < max(d, v_d) <= 256 on MFMA (fa_f64.hip: four waves of 16 queries /
+# keys, 16-column tiles, dK / dV in channel quarters and dQ in halves per launch; every rule, any
+# alignment and length)
+@pytest.mark.parametrize("d,vd", [(256, 256), (160, 160), (130, 200), (200, 64), (64, 256)])
+@pytest.mark.parametrize("policy,seq,mode,qs,ks,ws,ls,causal", [
+    ("full", 1, "none_front", (131,), (197,), 1, 1, False),
+    ("causal", 1, "scale_end", (150,), (75,), 1, 1, False),
+    ("local", 1, "scale_front", (120,), (241,), 40, 1, True),
+    ("local", 1, "none_front", (150,), (150,), 20, 3, False),
+    ("local", 2, "none_front", (9, 14), (9, 14), 4, 2, True),
+])
+def test_wide_channels_mfma_f64(d, vd, policy, seq, mode, qs, ks, ws, ls, causal):
+    run_case(np.float64, policy, seq, mode, (2,), d, vd, qs, ks, ws=ws, ls=ls, causal=causal, seed=d + 13 * vd)
 
 
 # fp16 backward for 128 < max(d, v_d) <= 256 on MFMA (fa_bwd_f16_fast.hip launch_bwd_wide: the one-wave

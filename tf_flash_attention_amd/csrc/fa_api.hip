@@ -381,7 +381,7 @@ const char* fa_last_error(void) { return g_last_error.c_str(); }
 #endif
 
 const char* fa_build_info(void) {
-  return "tf_flash_attention_amd: src=" FA_SRC_HASH "; lib=" FA_LIB_KIND "; gfx950; fwd={mfma_f16, mfma_f32, mfma_f64, generic(f16,f32,f64)}; bwd={mfma_f16 (two-pass / single-pass), mfma_f32 (two-pass), mfma_f64 (two-pass, d<=128), generic(f16,f32,f64)}";
+  return "tf_flash_attention_amd: src=" FA_SRC_HASH "; lib=" FA_LIB_KIND "; gfx950; fwd={mfma_f16, mfma_f32, mfma_f64, generic(f16,f32,f64)}; bwd={mfma_f16 (two-pass / single-pass), mfma_f32 (two-pass), mfma_f64 (two-pass, d<=256), generic(f16,f32,f64)}";
 }
 
 }  // extern "C"

@@ -23,6 +23,10 @@
 // transposed images then fits LDS) and the dK/dV pass runs twice, each launch accumulating one
 // half of the channels (the resident K', V operands plus all 128 channels of dK and dV would not
 // fit two waves per SIMD): the S / dP products are formed in both launches.
+// At 128 < D <= 256 every kernel runs four waves (one per SIMD, the whole 512-entry register file:
+// the resident operands alone are 128 registers a tensor) over 64-query (key) blocks and 16-column
+// tiles; the backward passes hold a quarter (dK / dV) or half (dQ) of their output channels per
+// launch and stage one tile at a time (a tile's four images are 132 KB).
 // Row images ([channel][32 keys|queries]) swap their 16-column halves on odd
 // channel rows so the four lane groups of an A-operand read hit disjoint banks;
 // transposed images ([32][D+16]) are padded for the same reason.
@@ -37,8 +41,9 @@ typedef double doublex2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) double lds_d_t;
 typedef __attribute__((address_space(3))) doublex2 lds_d2_t;
 
-constexpr int kThr = 512;   // 8 waves x 16 queries (keys)
-constexpr int kBM = 128;    // queries (keys) per workgroup
+// NW waves a workgroup, each 16 queries (keys): 8 up to D = 128, 4 past it
+template <int NW> constexpr int thr_of() { return 64 * NW; }
+template <int NW> constexpr int bm_of() { return 16 * NW; }
 constexpr int kT = 32;      // streamed keys (queries) per tile
 constexpr int kThrPrep = 256;
 constexpr double kRebase = 16.0;  // lazy max rebase threshold (natural units)
@@ -78,8 +83,9 @@ __device__ __forceinline__ bool vec_ok(int n, const void* p0, const void* p1) {
 // Streams tensors A [da][n] and B [db][n] in kT-column tiles: row image of A, row image
 // of B (kRB), transposed images ([kT][D+16]) of A (kTA) and B (kTB).  Register-staged
 // one tile ahead.
-template <int D, bool kRB, bool kTA, bool kTB, int TT = kT>
+template <int D, bool kRB, bool kTA, bool kTB, int TT = kT, int NW = 8>
 struct Stream64 {
+  static constexpr int kThr = thr_of<NW>();
   static constexpr int kP = D + 16;
   static constexpr int offA = 0, offB = D * TT, offAT = offB + (kRB ? D * TT : 0);
   static constexpr int offBT = offAT + (kTA ? TT * kP : 0);
@@ -106,27 +112,55 @@ struct Stream64 {
       reg[j] = v;
     }
   }
+  __device__ static void put(lds_d_t* slot, int idx, doublex2 v) {
+    if (idx < 2 * kChunks) {
+      const bool isB = idx >= kChunks;
+      const int k = isB ? idx - kChunks : idx, c = k / kCR, m = k % kCR;
+      if (!isB || kRB) *reinterpret_cast<lds_d2_t*>(slot + (isB ? offB : offA) + rimg<TT>(c, 2 * m)) = v;
+      if (isB ? kTB : kTA) {
+        lds_d_t* tr = slot + (isB ? offBT : offAT);
+        tr[(2 * m) * kP + c] = v[0];
+        tr[(2 * m + 1) * kP + c] = v[1];
+      }
+    }
+  }
   __device__ void store(lds_d_t* slot) const {
 #pragma unroll
-    for (int j = 0; j < kCPT; ++j) {
-      const int idx = threadIdx.x + kThr * j;
-      if (idx < 2 * kChunks) {
-        const bool isB = idx >= kChunks;
-        const int k = isB ? idx - kChunks : idx, c = k / kCR, m = k % kCR;
-        if (!isB || kRB) *reinterpret_cast<lds_d2_t*>(slot + (isB ? offB : offA) + rimg<TT>(c, 2 * m)) = reg[j];
-        if (isB ? kTB : kTA) {
-          lds_d_t* tr = slot + (isB ? offBT : offAT);
-          tr[(2 * m) * kP + c] = reg[j][0];
-          tr[(2 * m + 1) * kP + c] = reg[j][1];
+    for (int j = 0; j < kCPT; ++j) put(slot, threadIdx.x + kThr * j, reg[j]);
+  }
+  // the tile at col0 straight into slot, four chunks a thread at a time (no staging registers
+  // live beyond the group)
+  __device__ void copy(lds_d_t* slot, int col0) const {
+#pragma unroll 1
+    for (int j0 = 0; j0 < kCPT; j0 += 4) {
+      doublex2 v[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int idx = threadIdx.x + kThr * (j0 + jj);
+        v[jj] = doublex2{0.0, 0.0};
+        if (j0 + jj < kCPT && idx < 2 * kChunks) {
+          const bool isB = idx >= kChunks;
+          const int k = isB ? idx - kChunks : idx, c = k / kCR, m = k % kCR;
+          if (c < (isB ? db : da)) v[jj] = load2((isB ? B : A) + (int64_t)c * n, col0 + 2 * m, n, vec);
         }
       }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        if (j0 + jj < kCPT) put(slot, threadIdx.x + kThr * (j0 + jj), v[jj]);
     }
   }
 };
 
+// ring slots of a streamed tile: up to D = 128 two (register-staged one tile ahead, stored beside
+// the compute); past it one, loaded and stored between two barriers (the staging registers of a
+// 256-channel tile, 64 a lane, would spill the resident operands)
+constexpr int kLdsBytes = 160 * 1024;
+template <int D> constexpr int slots_of() { return D <= 128 ? 2 : 1; }
+
 // resident operand: X[c = 4s + g][col0 + 16w + r] of a [dx][n] tensor via an LDS [D][128] image
-template <int D>
+template <int D, int NW>
 __device__ __forceinline__ void stage_block(lds_d_t* img, const double* X, int dx, int n, int col0, bool vec) {
+  constexpr int kThr = thr_of<NW>(), kBM = bm_of<NW>();
   for (int idx = threadIdx.x; idx < D * (kBM / 2); idx += kThr) {
     const int c = idx / (kBM / 2), m = idx % (kBM / 2);
     doublex2 v = {0.0, 0.0};
@@ -138,11 +172,13 @@ __device__ __forceinline__ void stage_block(lds_d_t* img, const double* X, int d
 // ---------------------------------------------------------------------------
 // forward: 8 waves x 16 queries; key tiles of 32 (K row image + V transposed image)
 //   POL 0 full, 1 interval rules, 2 any other rule (per-element order check)
-template <int D, int POL>
-__global__ __launch_bounds__(kThr, 2) void fwd_f64_kernel(FwdArgs a) {
+template <int D, int POL, int NW, int TT>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 2 : 1) void fwd_f64_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_d_t* smem = (lds_d_t*)smem_raw;
-  using St = Stream64<D, false, false, true>;
+  constexpr int kBM = bm_of<NW>();
+  constexpr int kNT = TT / 16;  // 16-key blocks per tile
+  using St = Stream64<D, false, false, true, TT, NW>;
   const double kNegInf = -__builtin_huge_val();
   const int nq = a.rule.q.n, nk = a.rule.k.n, d = a.d, vd = a.v_d;
   const uint32_t nqb = (nq + kBM - 1) / kBM;
@@ -155,7 +191,7 @@ __global__ __launch_bounds__(kThr, 2) void fwd_f64_kernel(FwdArgs a) {
   const double sc = a.scale;
   const double* Q = static_cast<const double*>(a.Q) + bi * (int64_t)d * nq;
 
-  stage_block<D>(smem, Q, d, nq, q0, vec_ok(nq, a.Q, a.Q));
+  stage_block<D, NW>(smem, Q, d, nq, q0, vec_ok(nq, a.Q, a.Q));
   __syncthreads();
   double qf[D / 4];  // B operand of Sᵀ: Q[c = 4s + g][q = 16w + r] * scale
 #pragma unroll
@@ -165,8 +201,8 @@ __global__ __launch_bounds__(kThr, 2) void fwd_f64_kernel(FwdArgs a) {
   const int qlast = min(q0 + kBM, nq) - 1;
   int kb = 0, ke = nk;
   if (POL != 0) k_range_for_q_block(a.rule, q0, qlast, &kb, &ke);
-  const int kt0 = (kb / kT) * kT;
-  const int ntiles = (ke > kb) ? (ke - kt0 + kT - 1) / kT : 0;
+  const int kt0 = (kb / TT) * TT;
+  const int ntiles = (ke > kb) ? (ke - kt0 + TT - 1) / TT : 0;
   const int wq0 = q0 + 16 * w, wq1 = min(wq0 + 15, nq - 1);
   const bool wave_active = wq0 < nq;
   const int qi = wq0 + r;
@@ -191,14 +227,20 @@ __global__ __launch_bounds__(kThr, 2) void fwd_f64_kernel(FwdArgs a) {
   double m_run = 0.0, l_run = 0.0, m_max = kNegInf;
   bool m_set = false;
 
-  if (ntiles > 0) st.load(kt0);
+  constexpr int kSlots = slots_of<D>();
+  if (kSlots == 2 && ntiles > 0) st.load(kt0);
   for (int it = 0; it < ntiles; ++it) {
-    const int k0 = kt0 + it * kT;
-    st.store(smem + (it & 1) * St::kSlot);
-    if (it + 1 < ntiles) st.load(k0 + kT);
+    const int k0 = kt0 + it * TT;
+    if constexpr (kSlots == 2) {
+      st.store(smem + (it & 1) * St::kSlot);
+      if (it + 1 < ntiles) st.load(k0 + TT);
+    } else {
+      __syncthreads();
+      st.copy(smem, k0);
+    }
     __syncthreads();
 
-    const int k1 = k0 + kT - 1;
+    const int k1 = k0 + TT - 1;
     int cls;
     if (!wave_active) cls = 0;
     else if (POL == 0) cls = k1 < nk ? 2 : 1;
@@ -208,18 +250,19 @@ __global__ __launch_bounds__(kThr, 2) void fwd_f64_kernel(FwdArgs a) {
       if (cls == 2 && k1 >= nk) cls = 1;
     }
     if (cls == 0) continue;
-    const lds_d_t* base = smem + (it & 1) * St::kSlot;
+    const lds_d_t* base = smem + (kSlots == 2 ? (it & 1) : 0) * St::kSlot;
 
     // Sᵀ - m: A = Kᵀ (lane: key 16t + r, channel 4s + g)
-    doublex4 s4[2];
-    s4[0] = s4[1] = splat4(-m_run);
+    doublex4 s4[kNT];
+#pragma unroll
+    for (int t = 0; t < kNT; ++t) s4[t] = splat4(-m_run);
 #pragma unroll
     for (int s = 0; s < D / 4; ++s)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) s4[t] = mma(base[St::offA + rimg(4 * s + g, 16 * t + r)], qf[s], s4[t]);
+      for (int t = 0; t < kNT; ++t) s4[t] = mma(base[St::offA + rimg<TT>(4 * s + g, 16 * t + r)], qf[s], s4[t]);
     if (cls == 1) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < kNT; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key = k0 + 16 * t + g + 4 * i;
@@ -232,8 +275,9 @@ __global__ __launch_bounds__(kThr, 2) void fwd_f64_kernel(FwdArgs a) {
           s4[t][i] = ok ? s4[t][i] : kNegInf;
         }
     }
-    double mt = fmax(fmax(fmax(s4[0][0], s4[0][1]), fmax(s4[0][2], s4[0][3])),
-                     fmax(fmax(s4[1][0], s4[1][1]), fmax(s4[1][2], s4[1][3])));
+    double mt = fmax(fmax(s4[0][0], s4[0][1]), fmax(s4[0][2], s4[0][3]));
+#pragma unroll
+    for (int t = 1; t < kNT; ++t) mt = fmax(mt, fmax(fmax(s4[t][0], s4[t][1]), fmax(s4[t][2], s4[t][3])));
     mt = grp_max(mt);
     m_max = fmax(m_max, m_run + mt);
     const bool seed = !m_set && (mt != kNegInf);
@@ -245,11 +289,11 @@ __global__ __launch_bounds__(kThr, 2) void fwd_f64_kernel(FwdArgs a) {
       l_run *= alpha;
 #pragma unroll
       for (int u = 0; u < D / 16; ++u) acc[u] *= alpha;
-      s4[0] -= delta;
-      s4[1] -= delta;
+#pragma unroll
+      for (int t = 0; t < kNT; ++t) s4[t] -= delta;
     }
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < kNT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         s4[t][i] = exp(s4[t][i]);
@@ -257,7 +301,7 @@ __global__ __launch_bounds__(kThr, 2) void fwd_f64_kernel(FwdArgs a) {
       }
     // Oᵀ[v][q] += Σ_key V[v][key] P[key][q]: k-step (t, i) = keys 16t + 4i + g
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < kNT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const lds_d_t* vrow = base + St::offBT + (16 * t + 4 * i + g) * St::kP + r;
@@ -315,22 +359,23 @@ __global__ __launch_bounds__(kThrPrep) void bwd_prep_f64_kernel(BwdArgs a) {
   static_cast<double*>(a.ws_lse)[i] = (l > 0.0) ? m + log(l) : __builtin_huge_val();
 }
 
-// D <= 64: the resident K and V (Q and dO) blocks are staged together; at D = 128 one after the other
-template <int D, int TT>
+// D <= 64: the resident K and V (Q and dO) blocks are staged together; above one after the other
+template <int D, int TT, int NW, typename St>
 constexpr int bwd64_smem() {
-  constexpr int s1 = 2 * Stream64<D, true, true, true, TT>::kSlot, s2 = (D > 64 ? 1 : 2) * D * kBM;
+  constexpr int s1 = slots_of<D>() * St::kSlot, s2 = (D > 64 ? 1 : 2) * D * bm_of<NW>();
   return 8 * (s1 > s2 ? s1 : s2);
 }
 
 // resident B operands X[c = 4s + g][col0 + 16w + r] (x scale) of two tensors, through LDS: both images
 // at once for D <= 64, one at a time above (a [128][128] double image is 128 KB)
-template <int D>
+template <int D, int NW>
 __device__ __forceinline__ void resident_pair(lds_d_t* smem, const double* X, int dx, const double* Y, int dy, int n,
                                               int col0, bool vec, double xs, double (&xf)[D / 4], double (&yf)[D / 4]) {
+  constexpr int kBM = bm_of<NW>();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
   if constexpr (D <= 64) {
-    stage_block<D>(smem, X, dx, n, col0, vec);
-    stage_block<D>(smem + D * kBM, Y, dy, n, col0, vec);
+    stage_block<D, NW>(smem, X, dx, n, col0, vec);
+    stage_block<D, NW>(smem + D * kBM, Y, dy, n, col0, vec);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < D / 4; ++s) {
@@ -338,12 +383,12 @@ __device__ __forceinline__ void resident_pair(lds_d_t* smem, const double* X, in
       yf[s] = smem[D * kBM + (4 * s + g) * kBM + 16 * w + r];
     }
   } else {
-    stage_block<D>(smem, X, dx, n, col0, vec);
+    stage_block<D, NW>(smem, X, dx, n, col0, vec);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < D / 4; ++s) xf[s] = smem[(4 * s + g) * kBM + 16 * w + r] * xs;
     __syncthreads();
-    stage_block<D>(smem, Y, dy, n, col0, vec);
+    stage_block<D, NW>(smem, Y, dy, n, col0, vec);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < D / 4; ++s) yf[s] = smem[(4 * s + g) * kBM + 16 * w + r];
@@ -351,16 +396,18 @@ __device__ __forceinline__ void resident_pair(lds_d_t* smem, const double* X, in
   __syncthreads();
 }
 
-// dK / dV: 8 waves x 16 keys; query tiles of TT (Q, dO row + transposed images, lse, D).
-// CH < 0: every channel of dK / dV; CH = 0 / 1: channels [CH·D/2, CH·D/2 + D/2) only
-template <int D, int POL, int TT = kT, int CH = -1>
-__global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
+// dK / dV: NW waves x 16 keys; query tiles of TT (Q, dO row + transposed images, lse, D).
+// Channels [CH·D/NCH, (CH + 1)·D/NCH) of dK / dV (NCH = 1: every channel)
+template <int D, int POL, int TT, int CH, int NCH, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_d_t* smem = (lds_d_t*)smem_raw;
-  using St = Stream64<D, true, true, true, TT>;
+  constexpr int kBM = bm_of<NW>();
+  using St = Stream64<D, true, true, true, TT, NW>;
   constexpr int kNT = TT / 16;                      // 16-query blocks per tile
-  constexpr int kNU = (CH < 0 ? D : D / 2) / 16;    // 16-channel blocks of dK / dV held
-  constexpr int kC0 = CH < 0 ? 0 : CH * (D / 2);    // first channel held
+  constexpr int kNU = D / NCH / 16;                 // 16-channel blocks of dK / dV held
+  constexpr int kC0 = CH * (D / NCH);               // first channel held
+  constexpr int kSlots = slots_of<D>();
   const int nq = a.rule.q.n, nk = a.rule.k.n, d = a.d, vd = a.v_d;
   const uint32_t nkb = (nk + kBM - 1) / kBM;
   const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -376,7 +423,7 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
   const double* gD = static_cast<const double*>(a.ws_D) + bi * (int64_t)nq;
 
   double kb[D / 4], vb[D / 4];  // B operands: X[c = 4s + g][key = k0 + 16w + r]
-  resident_pair<D>(smem, K, d, V, vd, nk, k0, vec_ok(nk, a.K, a.V), sc, kb, vb);
+  resident_pair<D, NW>(smem, K, d, V, vd, nk, k0, vec_ok(nk, a.K, a.V), sc, kb, vb);
 
   const int klast = min(k0 + kBM, nk) - 1;
   int qb = 0, qe = nq;
@@ -414,18 +461,30 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
 #pragma unroll
   for (int u = 0; u < kNU; ++u) dk[u] = dv[u] = splat4(0.0);
 
-  if (ntiles > 0) { load_tile(qt0); store_tile(0); }
-  if (ntiles > 1) load_tile(qt0 + TT);
+  if (kSlots == 2 && ntiles > 0) {
+    load_tile(qt0);
+    store_tile(0);
+  }
+  if (kSlots == 2 && ntiles > 1) load_tile(qt0 + TT);
   for (int it = 0; it < ntiles; ++it) {
     __syncthreads();
     const int qa = qt0 + it * TT;
-    if (it + 1 < ntiles) store_tile((it + 1) & 1);
-    if (it + 2 < ntiles) load_tile(qa + 2 * TT);
+    if constexpr (kSlots == 2) {
+      if (it + 1 < ntiles) store_tile((it + 1) & 1);
+      if (it + 2 < ntiles) load_tile(qa + 2 * TT);
+    } else {  // one slot: this tile copied in between two barriers
+      st.copy(smem, qa);
+      if (tid < 2 * TT) {
+        const int q = qa + (tid & (TT - 1));
+        smem[St::offC + tid] = (q < nq) ? ((tid < TT) ? glse[q] : gD[q]) : ((tid < TT) ? __builtin_huge_val() : 0.0);
+      }
+      __syncthreads();
+    }
     int cls = 2;
     if (!wave_active) cls = 0;
     else if (POL != 0) cls = tile_class(a.rule, qa, min(qa + TT, nq) - 1, wk0, wk1);
     if (cls == 0) continue;
-    const lds_d_t* base = smem + (it & 1) * St::kSlot;
+    const lds_d_t* base = smem + (kSlots == 2 ? (it & 1) : 0) * St::kSlot;
     doublex4 sacc[kNT], pacc[kNT];
 #pragma unroll
     for (int t = 0; t < kNT; ++t)
@@ -486,13 +545,18 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dkdv_f64_kernel(BwdArgs a) {
     }
 }
 
-// dQ: 8 waves x 16 queries; key tiles of TT (K, V row images + K transposed image)
-template <int D, int POL, int TT = kT>
-__global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
+// dQ: NW waves x 16 queries; key tiles of TT (K, V row images + K transposed image).
+// Channels [CH·D/NCH, (CH + 1)·D/NCH) of dQ
+template <int D, int POL, int TT, int CH, int NCH, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void bwd_dq_f64_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_d_t* smem = (lds_d_t*)smem_raw;
-  using St = Stream64<D, true, true, false, TT>;
+  constexpr int kBM = bm_of<NW>();
+  using St = Stream64<D, true, true, false, TT, NW>;
   constexpr int kNT = TT / 16;  // 16-key blocks per tile
+  constexpr int kNU = D / NCH / 16;  // 16-channel blocks of dQ held
+  constexpr int kC0 = CH * (D / NCH);
+  constexpr int kSlots = slots_of<D>();
   const double kNegInf = -__builtin_huge_val();
   const int nq = a.rule.q.n, nk = a.rule.k.n, d = a.d, vd = a.v_d;
   const uint32_t nqb = (nq + kBM - 1) / kBM;
@@ -507,7 +571,7 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
   const double* dO = static_cast<const double*>(a.dO) + bi * (int64_t)vd * nq;
 
   double qf[D / 4], of[D / 4];  // B operands: X[c = 4s + g][q = q0 + 16w + r]
-  resident_pair<D>(smem, Q, d, dO, vd, nq, q0, vec_ok(nq, a.Q, a.dO), sc, qf, of);
+  resident_pair<D, NW>(smem, Q, d, dO, vd, nq, q0, vec_ok(nq, a.Q, a.dO), sc, qf, of);
 
   const int wq0 = q0 + 16 * w, wq1 = min(wq0 + 15, nq - 1);
   const int qi = wq0 + r;
@@ -534,17 +598,25 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
 
   St st{static_cast<const double*>(a.K) + bi * (int64_t)d * nk, static_cast<const double*>(a.V) + bi * (int64_t)vd * nk,
         d, vd, nk, vec_ok(nk, a.K, a.V), {}};
-  doublex4 dq[D / 16];
+  doublex4 dq[kNU];
 #pragma unroll
-  for (int u = 0; u < D / 16; ++u) dq[u] = splat4(0.0);
+  for (int u = 0; u < kNU; ++u) dq[u] = splat4(0.0);
 
-  if (ntiles > 0) { st.load(kt0); st.store(smem); }
-  if (ntiles > 1) st.load(kt0 + TT);
+  if (kSlots == 2 && ntiles > 0) {
+    st.load(kt0);
+    st.store(smem);
+  }
+  if (kSlots == 2 && ntiles > 1) st.load(kt0 + TT);
   for (int it = 0; it < ntiles; ++it) {
     __syncthreads();
     const int ka = kt0 + it * TT;
-    if (it + 1 < ntiles) st.store(smem + ((it + 1) & 1) * St::kSlot);
-    if (it + 2 < ntiles) st.load(ka + 2 * TT);
+    if constexpr (kSlots == 2) {
+      if (it + 1 < ntiles) st.store(smem + ((it + 1) & 1) * St::kSlot);
+      if (it + 2 < ntiles) st.load(ka + 2 * TT);
+    } else {
+      st.copy(smem, ka);
+      __syncthreads();
+    }
     int cls;
     if (!wave_active) cls = 0;
     else if (POL == 0) cls = (ka + TT <= nk) ? 2 : 1;
@@ -553,7 +625,7 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
       if (cls == 2 && ka + TT > nk) cls = 1;
     }
     if (cls == 0) continue;
-    const lds_d_t* base = smem + (it & 1) * St::kSlot;
+    const lds_d_t* base = smem + (kSlots == 2 ? (it & 1) : 0) * St::kSlot;
     doublex4 sacc[kNT], pacc[kNT];
 #pragma unroll
     for (int t = 0; t < kNT; ++t) {
@@ -587,98 +659,116 @@ __global__ __launch_bounds__(kThr, 1) void bwd_dq_f64_kernel(BwdArgs a) {
     for (int t = 0; t < kNT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const lds_d_t* krow = base + St::offAT + (16 * t + 4 * i + g) * St::kP + r;
+        const lds_d_t* krow = base + St::offAT + (16 * t + 4 * i + g) * St::kP + kC0 + r;
 #pragma unroll
-        for (int u = 0; u < D / 16; ++u) dq[u] = mma(krow[16 * u], ds[t][i], dq[u]);
+        for (int u = 0; u < kNU; ++u) dq[u] = mma(krow[16 * u], ds[t][i], dq[u]);
       }
   }
 
   if (!wave_active || qi >= nq) return;
   double* dQ = static_cast<double*>(a.dQ) + bi * (int64_t)d * nq;
 #pragma unroll
-  for (int u = 0; u < D / 16; ++u)
+  for (int u = 0; u < kNU; ++u)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = 16 * u + g + 4 * i;
+      const int c = kC0 + 16 * u + g + 4 * i;
       if (c < d) dQ[(int64_t)c * nq + qi] = dq[u][i] * sc;
     }
 }
 
 int policy_class(const Rule& r) { return r.policy == 0 ? 0 : (rule_is_interval(r) ? 1 : 2); }
 
+// NW = 8 waves and 32-column tiles up to D = 64, 16-column tiles at D = 128; 4 waves past it
+template <int D> constexpr int nw_of() { return D > 128 ? 4 : 8; }
+template <int D> constexpr int tt_of() { return D > 64 ? 16 : kT; }
+
 template <int D>
 hipError_t launch_fwd_t(const FwdArgs& a, hipStream_t s) {
-  constexpr int sm1 = 2 * Stream64<D, false, false, true>::kSlot, sm2 = D * kBM;
+  constexpr int NW = nw_of<D>(), TT = D > 128 ? 16 : kT;
+  using St = Stream64<D, false, false, true, TT, NW>;
+  constexpr int sm1 = slots_of<D>() * St::kSlot, sm2 = D * bm_of<NW>();
   constexpr int smem = 8 * (sm1 > sm2 ? sm1 : sm2);
+  static_assert(smem <= kLdsBytes, "fp64 forward: LDS");
   const int pol = policy_class(a.rule);
-  auto kern = pol == 0 ? fwd_f64_kernel<D, 0> : (pol == 1 ? fwd_f64_kernel<D, 1> : fwd_f64_kernel<D, 2>);
+  auto kern = pol == 0 ? fwd_f64_kernel<D, 0, NW, TT>
+                       : (pol == 1 ? fwd_f64_kernel<D, 1, NW, TT> : fwd_f64_kernel<D, 2, NW, TT>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), smem);
   if (e != hipSuccess) return e;
-  const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kThr), smem, s, a);
+  const int64_t nqb = (a.rule.q.n + bm_of<NW>() - 1) / bm_of<NW>();
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(thr_of<NW>()), smem, s, a);
   return hipGetLastError();
 }
 
-template <int D, int TT = kT, int CH = -1>
+template <int D, int CH, int NCH>
 hipError_t launch_dkdv_f64(const BwdArgs& a, hipStream_t s) {
+  constexpr int NW = nw_of<D>(), TT = tt_of<D>();
   const int pol = policy_class(a.rule);
-  auto kk = pol == 0 ? bwd_dkdv_f64_kernel<D, 0, TT, CH>
-                     : (pol == 1 ? bwd_dkdv_f64_kernel<D, 1, TT, CH> : bwd_dkdv_f64_kernel<D, 2, TT, CH>);
-  constexpr int smem = bwd64_smem<D, TT>();
+  auto kk = pol == 0 ? bwd_dkdv_f64_kernel<D, 0, TT, CH, NCH, NW>
+                     : (pol == 1 ? bwd_dkdv_f64_kernel<D, 1, TT, CH, NCH, NW> : bwd_dkdv_f64_kernel<D, 2, TT, CH, NCH, NW>);
+  constexpr int smem = bwd64_smem<D, TT, NW, Stream64<D, true, true, true, TT, NW>>();
+  static_assert(smem <= kLdsBytes, "fp64 dK/dV: LDS");
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kk), smem);
   if (e != hipSuccess) return e;
-  const int64_t nkb = (a.rule.k.n + kBM - 1) / kBM;
-  hipLaunchKernelGGL(kk, dim3((unsigned)(a.b * nkb)), dim3(kThr), smem, s, a);
+  const int64_t nkb = (a.rule.k.n + bm_of<NW>() - 1) / bm_of<NW>();
+  hipLaunchKernelGGL(kk, dim3((unsigned)(a.b * nkb)), dim3(thr_of<NW>()), smem, s, a);
   return hipGetLastError();
 }
 
-template <int D, int TT = kT>
+template <int D, int CH, int NCH>
 hipError_t launch_dq_f64(const BwdArgs& a, hipStream_t s) {
+  constexpr int NW = nw_of<D>(), TT = tt_of<D>();
   const int pol = policy_class(a.rule);
-  auto kq = pol == 0 ? bwd_dq_f64_kernel<D, 0, TT> : (pol == 1 ? bwd_dq_f64_kernel<D, 1, TT> : bwd_dq_f64_kernel<D, 2, TT>);
-  constexpr int smem = bwd64_smem<D, TT>();
+  auto kq = pol == 0 ? bwd_dq_f64_kernel<D, 0, TT, CH, NCH, NW>
+                     : (pol == 1 ? bwd_dq_f64_kernel<D, 1, TT, CH, NCH, NW> : bwd_dq_f64_kernel<D, 2, TT, CH, NCH, NW>);
+  constexpr int smem = bwd64_smem<D, TT, NW, Stream64<D, true, true, false, TT, NW>>();
+  static_assert(smem <= kLdsBytes, "fp64 dQ: LDS");
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kq), smem);
   if (e != hipSuccess) return e;
-  const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
-  hipLaunchKernelGGL(kq, dim3((unsigned)(a.b * nqb)), dim3(kThr), smem, s, a);
+  const int64_t nqb = (a.rule.q.n + bm_of<NW>() - 1) / bm_of<NW>();
+  hipLaunchKernelGGL(kq, dim3((unsigned)(a.b * nqb)), dim3(thr_of<NW>()), smem, s, a);
   return hipGetLastError();
 }
 
+// channel chunks a launch holds: dK / dV all up to D = 64, halves at 128, quarters at 256 (the
+// resident K', V operands take 2·D/4 doubles a lane); dQ all up to 128, halves at 256
 template <int D>
 hipError_t launch_bwd_t(const BwdArgs& a, hipStream_t s) {
-  hipError_t e;
-  if constexpr (D <= 64) {
-    e = launch_dkdv_f64<D>(a, s);
-    if (e != hipSuccess) return e;
-    return launch_dq_f64<D>(a, s);
-  } else {  // 16-column tiles; dK / dV in two channel halves
-    e = launch_dkdv_f64<D, 16, 0>(a, s);
-    if (e != hipSuccess) return e;
-    e = launch_dkdv_f64<D, 16, 1>(a, s);
-    if (e != hipSuccess) return e;
-    return launch_dq_f64<D, 16>(a, s);
+  constexpr int NKV = D <= 64 ? 1 : (D <= 128 ? 2 : 4), NQ = D <= 128 ? 1 : 2;
+  hipError_t e = launch_dkdv_f64<D, 0, NKV>(a, s);
+  if constexpr (NKV > 1) {
+    if (e == hipSuccess) e = launch_dkdv_f64<D, 1, NKV>(a, s);
   }
+  if constexpr (NKV > 2) {
+    if (e == hipSuccess) e = launch_dkdv_f64<D, 2, NKV>(a, s);
+    if (e == hipSuccess) e = launch_dkdv_f64<D, 3, NKV>(a, s);
+  }
+  if (e == hipSuccess) e = launch_dq_f64<D, 0, NQ>(a, s);
+  if constexpr (NQ > 1) {
+    if (e == hipSuccess) e = launch_dq_f64<D, 1, NQ>(a, s);
+  }
+  return e;
 }
 
 }  // namespace
 
 bool fwd_f64_supported(const FwdArgs& a) {
-  return a.d >= 1 && a.v_d >= 1 && a.d <= 128 && a.v_d <= 128 && a.b * ((a.rule.q.n + kBM - 1) / kBM) < (1ll << 31);
+  return a.d >= 1 && a.v_d >= 1 && a.d <= 256 && a.v_d <= 256 && a.b * ((a.rule.q.n + 63) / 64) < (1ll << 31);
 }
 
 hipError_t launch_fwd_f64(const FwdArgs& a, hipStream_t s) {
   const int dm = max(a.d, a.v_d);
   if (dm <= 32) return launch_fwd_t<32>(a, s);
   if (dm <= 64) return launch_fwd_t<64>(a, s);
-  return launch_fwd_t<128>(a, s);
+  if (dm <= 128) return launch_fwd_t<128>(a, s);
+  return launch_fwd_t<256>(a, s);
 }
 
 // backward keeps K·scale, V (dkdv) or Q·scale, dO (dq) plus the dK/dV (dQ) accumulators in
-// registers: 2·D/4 + 2·D/16·4 doubles per lane up to D = 64; at D = 128 the dK/dV pass holds one
-// channel half per launch (2·32 + 2·16 doubles)
+// registers: 2·D/4 + 2·D/16·4 doubles per lane up to D = 64; past it the passes hold a channel chunk
+// of their outputs per launch (launch_bwd_t)
 bool bwd_f64_supported(const BwdArgs& a) {
-  return a.d >= 1 && a.v_d >= 1 && a.d <= 128 && a.v_d <= 128 && a.b * ((a.rule.k.n + kBM - 1) / kBM) < (1ll << 31) &&
-         a.b * ((a.rule.q.n + kBM - 1) / kBM) < (1ll << 31);
+  return a.d >= 1 && a.v_d >= 1 && a.d <= 256 && a.v_d <= 256 && a.b * ((a.rule.k.n + 63) / 64) < (1ll << 31) &&
+         a.b * ((a.rule.q.n + 63) / 64) < (1ll << 31);
 }
 
 hipError_t launch_bwd_f64(const BwdArgs& a, hipStream_t s) {
@@ -690,7 +780,8 @@ hipError_t launch_bwd_f64(const BwdArgs& a, hipStream_t s) {
   const int dm = max(a.d, a.v_d);
   if (dm <= 32) return launch_bwd_t<32>(a, s);
   if (dm <= 64) return launch_bwd_t<64>(a, s);
-  return launch_bwd_t<128>(a, s);
+  if (dm <= 128) return launch_bwd_t<128>(a, s);
+  return launch_bwd_t<256>(a, s);
 }
 
 }  // namespace fa

@@ -6,6 +6,9 @@ trace shows which kernels serve them:
 
 The two-pass backward (bwd_dkdv_kernel / bwd_dq_kernel) should be the only backward kernels in the
 trace: no bwd_f16_kernel (single-pass, atomics) and no bwd_generic_kernel.
+
+With the argument f64 it runs fp64 forward + backward at 128 < D <= 256 over every rule class instead
+(the trace should show fwd_f64_kernel / bwd_dkdv_f64_kernel / bwd_dq_f64_kernel and no *_generic_*).
 """
 import os
 import sys
@@ -27,15 +30,25 @@ SHAPES = [
 ]
 
 
+SHAPES_F64 = [
+    ("full", 1, 256, (131,), (197,), 1, 0, False, False),
+    ("causal", 1, 256, (150,), (150,), 1, 0, False, False),
+    ("local", 1, 200, (120,), (241,), 40, 0, True, False),
+    ("local", 2, 256, (9, 14), (9, 14), 4, 2, True, False),
+]
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    for policy, sd, d, qs, ks, ws, ls, causal, mis in SHAPES:
+    f64 = len(sys.argv) > 1 and sys.argv[1] == "f64"
+    dt = torch.float64 if f64 else torch.float16
+    for policy, sd, d, qs, ks, ws, ls, causal, mis in (SHAPES_F64 if f64 else SHAPES):
         def mk(shape):
             n = 1
             for x in shape:
                 n *= x
-            buf = (torch.rand(n + 1, generator=g, device=dev) * 4 - 2).half()
+            buf = (torch.rand(n + 1, generator=g, device=dev, dtype=torch.float64) * 4 - 2).to(dt)
             t = (buf[1:] if mis else buf[:n]).view(shape)
             return t.requires_grad_(True)
         q, k, v = mk((2, d) + qs), mk((2, d) + ks), mk((2, d) + ks)
