@@ -1,4 +1,4 @@
-"""Per-kernel summary (name, calls, total / average ns) of a rocprofv3 kernel-trace database, the
+"""Per-kernel summary (name, calls, total / average microseconds as the database reports them) of a rocprofv3 kernel-trace database, the
 framework's kernels only (names in namespace fa::).  Usage: python tools/trace_summary.py RUN_DIR [OUT_CSV]"""
 import csv
 import glob
@@ -14,7 +14,7 @@ def main():
     rows = [r for r in rows if "fa::" in r["name"]]
     out = open(sys.argv[2], "w", newline="") if len(sys.argv) > 2 else sys.stdout
     w = csv.writer(out)
-    w.writerow(["name", "calls", "total_ns", "average_ns"])
+    w.writerow(["name", "calls", "total_us", "average_us"])
     for r in rows:
         w.writerow([r["name"], r["total_calls"], round(r["total_duration"], 1), round(r["average"], 1)])
 
