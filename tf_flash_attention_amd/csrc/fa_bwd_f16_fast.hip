@@ -99,10 +99,9 @@ struct DkdvSmem {
 // pass, two waves per SIMD; d = 128 runs the producer / consumer pass below).
 // OC > 1 (128 < d <= 256): the workgroup accumulates dK / dV for one of OC chunks of D / OC output
 // channels (chunk = block index mod OC), forming S and dP over all D channels as before: the 256-channel
-// accumulators of both gradients would not fit one wave beside the resident K' and V.
-// RA: every LDS operand read two MFMA pairs ahead into a three-deep register rotation (diagnostic
-// variant 1420 at D = 256: measured slower there, hipcc's own placement stays).
-template <int D, int NW, int WPE, int POL, bool ALN, int OC = 1, bool RA = false>
+// accumulators of both gradients would not fit one wave beside the resident K' and V (round 4's D = 256
+// pass; the four-role pass below replaces it, FA_BWD_VARIANT=1421 keeps it for A/B).
+template <int D, int NW, int WPE, int POL, bool ALN, int OC = 1>
 __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -280,7 +279,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   };
   // S = Qᵀ·K', dP = dOᵀ·V: A operands (row q, k = channel) by transposed reads
   auto sdp = [&](const lds_char_t* base, floatx16& sacc, floatx16& pacc) {
-    constexpr int kAh = RA ? 2 : 0;
+    constexpr int kAh = 0;
     half8 qa8[kAh + 1], oa8[kAh + 1];
     auto rd = [&](int s) __attribute__((always_inline)) {
 #pragma unroll
@@ -332,7 +331,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
   };
   // dV += dO·P, dK += Q·dS: A = X[row 32u + r][queries 16s + 8h + 0..7] (b128 reads of the Q16 images)
   auto dvdk = [&](const lds_char_t* base, const half8 (&pf)[2], const half8 (&sf)[2]) {
-    constexpr int kU = kDO / 32, kN = 2 * kU, kAh = RA ? 2 : 0;
+    constexpr int kU = kDO / 32, kN = 2 * kU, kAh = 0;
     half8 oa[kAh + 1], qa[kAh + 1];
     auto rd = [&](int n) __attribute__((always_inline)) {  // product n = kU·s + u
       const int s = n / kU, u = n % kU;
@@ -767,6 +766,394 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       if (c < vd) dV[(int64_t)c * nk + key] = __float2half(dv[u][i]);
     }
 }
+
+// ---------------------------------------------------------------------------
+// dK / dV at D = 256 without the recomputed products: four roles a 32-key slice, each holding one
+// 64-register resident operand or one 128-register accumulator at two waves per SIMD
+//   A  (S):   S = Qᵀ·K' (C = -lse2), P = exp2(S) (masked)          -> P   hand-over
+//   B  (dP):  dP = dOᵀ·V (C = -D) of the tile before, dS = P∘dP      -> dS  hand-over
+//   C  (dV):  dV += dO·P of the tile before
+//   Dk (dK):  dK += Q·dS of the tile two before
+// so S and dP are formed once per (key block, query tile) instead of once per 128-channel output
+// chunk (the one-wave pass with OC = 2 issued 96 MFMAs a 32 x 32 pair; this pass 64, 16 a role).
+// A workgroup = two slices (64 keys); waves 0-3 = A0, B0, A1, B1 and 4-7 = C0, Dk0, C1, Dk1, so every
+// SIMD pairs a softmax role with an accumulating one.  Every step: one barrier, the staging of tile
+// it+1 into the four-slot ring (Q, dO Q16 images, -lse2, -D), the load of tile it+3.
+struct W4Smem {
+  static constexpr int D = 256;
+  static constexpr int kBK = 64;              // keys per workgroup: two slices of 32
+  static constexpr int kRow = D * kBK * 2;    // K (or V) row image (prologue only): 32 KB
+  static constexpr int kQT = D * 64;          // one [D][32] Q16 image: 16 KB
+  static constexpr int offQT = 0, offOT = kQT, offLse = 2 * kQT, offD = offLse + 128;
+  static constexpr int kSlot = offLse + 256;  // + -lse2[32], -D[32]
+  static constexpr int kNS = 4;               // query-tile ring
+  static constexpr int kXW = 2048;            // one slice's P (or dS) of a tile: 32 x 32 fp16, lane-linear
+  static constexpr int offP = kNS * kSlot;    // P hand-over: 2 slots x 2 slices
+  static constexpr int offS = offP + 4 * kXW; // dS hand-over: 2 slots x 2 slices
+  static constexpr int kUsed = offS + 4 * kXW;
+  static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;
+};
+
+template <int POL, bool ALN>
+__global__ __launch_bounds__(512, 1) void bwd_dkdv_w4_kernel(BwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char_t* smem = (lds_char_t*)smem_raw;
+  using S = W4Smem;
+  constexpr int D = S::D;
+  constexpr int kThr = 512;
+  constexpr int kBK = S::kBK;
+  constexpr int kQChunks = D * 4;                 // 16-B chunks of one [D][32] tile
+  constexpr int kCPT = 2 * kQChunks / kThr;       // Q and dO chunks per thread
+  const int nq = a.rule.q.n, nk = a.rule.k.n;
+  const uint32_t nkb = (nk + kBK - 1) / kBK;
+  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t bi = bid / nkb;
+  const int k0 = (int)(bid % nkb) * kBK;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sl = (w >> 1) & 1;                    // key slice
+  const int role = (w & 1) + 2 * (w >> 2);        // 0 A, 1 B, 2 C, 3 Dk
+  const int h = lane >> 5, r = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const int sig = ((tp & 1) << 1) | (tp >> 1);   // σ-permuted transposed reads (see the dK/dV kernel)
+  const float c2 = (float)a.scale * kLog2e;
+
+  const int d = a.d, vd = a.v_d;
+  const __half* K = static_cast<const __half*>(a.K) + bi * (int64_t)d * nk;
+  const __half* V = static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk;
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq, 2u * d * nq);
+  const __amdgpu_buffer_rsrc_t ors = make_rsrc(static_cast<const __half*>(a.dO) + bi * (int64_t)vd * nq, 2u * vd * nq);
+  const float* glse = static_cast<const float*>(a.ws_lse) + bi * (int64_t)nq;
+  const float* gD = static_cast<const float*>(a.ws_D) + bi * (int64_t)nq;
+
+  // ---- K, V blocks into LDS (every thread); roles A / B read their resident B operands below
+  {
+    constexpr int kRPT = 2 * D * (kBK / 8) / kThr, kHalf = D * (kBK / 8) / kThr;
+    static_assert(kHalf * kThr == D * (kBK / 8), "resident chunks must divide over the workgroup");
+    const __amdgpu_buffer_rsrc_t krs2 = make_rsrc(K, 2u * d * nk), vrs2 = make_rsrc(V, 2u * vd * nk);
+    u32x4 rv[kRPT];
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
+      const int c = j / (kBK / 8), m = j % (kBK / 8);
+      const bool in = c < (which ? vd : d) && k0 + 8 * m < nk;
+      if constexpr (ALN)
+        rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? vrs2 : krs2,
+                                                       in ? (uint32_t)c * (uint32_t)nk * 2u + 16u * m : 0x80000000u, 2 * k0, 0);
+      else
+        rv[jj] = buf_load8h(which ? vrs2 : krs2, (uint32_t)c * (uint32_t)nk * 2u, k0 + 8 * m, nk, c < (which ? vd : d));
+    }
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
+      const int c = j / (kBK / 8), m = j % (kBK / 8);
+      // (128-B rows, unswizzled: the images are read once per block)
+      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBK) + m * 16) = rv[jj];
+    }
+  }
+  __syncthreads();
+
+  // ---- query range of this key block; per-lane / per-wave query intervals of the slice's keys
+  const int klast = min(k0 + kBK, nk) - 1;
+  int qb = 0, qe = nq;
+  if (POL != 0) q_range_for_k_block(a.rule, k0, klast, &qb, &qe);
+  const int qt0 = (qb / 32) * 32;
+  const int ntiles = (qe > qb) ? (qe - qt0 + 31) / 32 : 0;
+  const int key = k0 + 32 * sl + r;
+  const int wk0 = k0 + 32 * sl;
+  const bool wave_active = wk0 < nk;
+  int qlo = 0, qspan = nq, wlo_min = 0, wlo_max = 0, whi_min = nq - 1, whi_max = nq - 1;
+  if (POL == 1 && wave_active) {
+    int qhi;
+    query_interval(a.rule, min(key, nk - 1), &qlo, &qhi);
+    qspan = max(qhi - qlo + 1, 0);
+    const int last = min(31, nk - 1 - wk0);
+    wlo_min = __builtin_amdgcn_readfirstlane(qlo);
+    whi_min = __builtin_amdgcn_readfirstlane(qhi);
+    wlo_max = __builtin_amdgcn_readlane(qlo, last);
+    whi_max = __builtin_amdgcn_readlane(qhi, last);
+  }
+  // class of tile t for this slice (0 outside [0, ntiles): phantom steps)
+  auto tcls = [&](int t) -> int {
+    if (t < 0 || t >= ntiles || !wave_active) return 0;
+    const int qa = qt0 + 32 * t, qz = qa + 31;
+    if (POL == 0) return 2;  // q >= nq rows carry -lse2 = -inf -> P = 0; keys >= nk are never stored
+    if (POL == 2) return qa < nq ? tile_class(a.rule, qa, min(qz, nq - 1), wk0, min(wk0 + 31, nk - 1)) : 0;
+    if (wlo_min > qz || whi_max < qa) return 0;
+    return (wlo_max <= qa && whi_min >= qz) ? 2 : 1;
+  };
+
+  // ---- query-tile staging, every thread (Q, dO chunks: 8 queries of one channel row)
+  uint32_t voff[kCPT];
+  int crow_[kCPT], cm_[kCPT];
+#pragma unroll
+  for (int j = 0; j < kCPT; ++j) {
+    const int idx = (tid + kThr * j) % kQChunks;
+    crow_[j] = idx >> 2;
+    cm_[j] = idx & 3;
+    voff[j] = (uint32_t)crow_[j] * (uint32_t)nq * 2u + (ALN ? 16u * cm_[j] : 0u);
+  }
+  u32x4 qr[2][kCPT];  // two staging sets: tile t in set t&1, loaded two steps before it is stored
+  float lr[2] = {0.f, 0.f};
+  auto is_o = [&](int j) -> bool { return j >= kQChunks / kThr; };
+  auto load_tile = [&](int qa, int set) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isO = is_o(j);
+      if constexpr (ALN) {
+        const bool out = qa + 8 * cm_[j] >= nq || crow_[j] >= (isO ? vd : d);
+        qr[set][j] = buf_load16(isO ? ors : qrs, voff[j], 2 * min(qa, nq), out);
+      } else {
+        qr[set][j] = buf_load8h(isO ? ors : qrs, voff[j], qa + 8 * cm_[j], nq, crow_[j] < (isO ? vd : d));
+      }
+    }
+    if (tid < 64) {  // lanes 0..31: -lse2, 32..63: -D
+      const int q = qa + (tid & 31);
+      lr[set] = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? -__builtin_huge_valf() : 0.f);
+    }
+  };
+  auto store_tile = [&](int slot, int set) __attribute__((always_inline)) {
+    lds_char_t* base = smem + slot * S::kSlot;
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isO = is_o(j);
+      *reinterpret_cast<lds_u32x4_t*>(base + (isO ? S::offOT : S::offQT) + q16_off(crow_[j], cm_[j])) = qr[set][j];
+    }
+    if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr[set];
+  };
+  // hand-over of this slice: two b128 per lane (k-steps 0 / 1), lane-linear
+  auto poff = [&](int xs, int j) -> uint32_t { return S::offP + (2 * xs + sl) * S::kXW + j * 1024 + lane * 16; };
+  auto soff = [&](int xs, int j) -> uint32_t { return S::offS + (2 * xs + sl) * S::kXW + j * 1024 + lane * 16; };
+
+  // Steps it = 0 .. ntiles + 1: A handles tile it, B and C tile it-1, Dk tile it-2.  Whole groups of
+  // four steps (ring slot it % 4, staging set (it+1) % 2, hand-over slot it % 2 compile-time); loads
+  // and stores unconditional (phantom tiles move zeros), so hipcc's vmcnt waits stay exact.
+  const int nsteps = ntiles + 2;
+  // (TAG: a distinct marker per role, so hipcc does not merge the roles' identical staging blocks into
+  // one shared block, which joins every role's live registers: 884 spilled VGPRs)
+  auto stage = [&](auto C_, auto TAG_, int it) __attribute__((always_inline)) {
+    constexpr int c = decltype(C_)::value;
+    asm volatile("; stage, role %0" ::"i"(decltype(TAG_)::value));
+    __syncthreads();
+    store_tile((c + 1) % 4, (c + 1) % 2);         // tile it+1 (loaded in step it-2)
+    load_tile(qt0 + 32 * (it + 3), (c + 1) % 2);  // tile it+3 into the set just stored
+  };
+  load_tile(qt0, 0);
+  auto stage0 = [&](auto TAG_) __attribute__((always_inline)) {
+    asm volatile("; stage 0, role %0" ::"i"(decltype(TAG_)::value));
+    __syncthreads();  // the K / V images are retired: the ring may overwrite them
+    store_tile(0, 0);
+    load_tile(qt0 + 32, 1);
+    load_tile(qt0 + 64, 0);
+  };
+  // the S / dP A operand of k-step s_ from a Q16 image (transposed reads)
+  auto read_op = [&](const lds_char_t* img, int s_) __attribute__((always_inline)) -> half8 {
+    half8 x;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const uint32_t off = q16_off(16 * s_ + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
+      const half4 t = tr_read(img + off);
+      if (e == 0) x.lo = t; else x.hi = t;
+    }
+    return x;
+  };
+  // the resident B operand of a role A / B wave: X[c = 16s + 8h + j][key] from the K or V image
+  auto resident = [&](int which, half8 (&xb)[D / 16]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s_ = 0; s_ < D / 16; ++s_)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int crow = 16 * s_ + 8 * (g >> 1) + 4 * e + tq;
+        const int col = 32 * sl + 16 * (g & 1) + 4 * tp;
+        const half4 x = tr_read(smem + which * S::kRow + crow * (2 * kBK) + col * 2);
+        if (e == 0) xb[s_].lo = x; else xb[s_].hi = x;
+      }
+  };
+  // a row constant (-lse2 or -D) of the tile in `base` as the initial accumulator
+  auto read_rowc = [&](const lds_char_t* base, int off, floatx16& acc) __attribute__((always_inline)) {
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {  // registers 4gq..4gq+3 = queries 16(gq>>1) + 8h + 4(gq&1) + 0..3
+      const int q4 = 16 * (gq >> 1) + 8 * h + 4 * (gq & 1);
+      const floatx4 v4 = *reinterpret_cast<const lds_f4_t*>(base + off + 4 * q4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[4 * gq + j] = v4[j];
+    }
+  };
+  // S / dP chain: 16 MFMAs, A operands two k-steps ahead
+  auto chain = [&](const lds_char_t* img, const half8 (&xb)[D / 16], floatx16& acc) __attribute__((always_inline)) {
+    constexpr int kS = D / 16, kAh = 2;
+    half8 a8[kAh + 1];
+#pragma unroll
+    for (int s_ = 0; s_ < kAh; ++s_) a8[s_] = read_op(img, s_);
+#pragma unroll
+    for (int s_ = 0; s_ < kS; ++s_) {
+      if (s_ + kAh < kS) a8[(s_ + kAh) % (kAh + 1)] = read_op(img, s_ + kAh);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8[s_ % (kAh + 1)], xb[s_], acc, 0, 0, 0);
+    }
+  };
+  // X += Y·Z: A = Y[row 32u + r][queries 16s + 8h + 0..7] (b128 reads of a Q16 image, two ahead), B = Z k-step s
+  auto accum = [&](const lds_char_t* img, const half8 (&z)[2], floatx16 (&acc)[D / 32]) __attribute__((always_inline)) {
+    constexpr int kU = D / 32, kN = 2 * kU, kAh = 2;
+    half8 y[kAh + 1];
+    auto rd = [&](int n) __attribute__((always_inline)) {
+      y[n % (kAh + 1)] = read_b128(img + q16_off(32 * (n % kU) + r, 2 * (n / kU) + h));
+    };
+#pragma unroll
+    for (int n = 0; n < kAh; ++n) rd(n);
+#pragma unroll
+    for (int n = 0; n < kN; ++n) {
+      if (n + kAh < kN) rd(n + kAh);
+      acc[n % kU] = __builtin_amdgcn_mfma_f32_32x32x16_f16(y[n % (kAh + 1)], z[n / kU], acc[n % kU], 0, 0, 0);
+    }
+  };
+
+  if (role == 0) {
+    // ================= A: S, P
+    half8 kb[D / 16];
+    resident(0, kb);
+#pragma unroll
+    for (int s_ = 0; s_ < D / 16; ++s_) kb[s_] = scale8(kb[s_], c2);  // S in log2 units straight out of the MFMA
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every image read done before the ring reuses it
+    stage0(IC<0>{});
+    const int ko = (POL == 2) ? seq_order(a.rule.k, a.rule, min(key, nk - 1)) : 0;
+    auto astep = [&](auto C_, int it) __attribute__((always_inline)) {
+      constexpr int c = decltype(C_)::value;
+      stage(C_, IC<0>{}, it);
+      const int cls = tcls(it);
+      if (cls == 0) return;
+      const lds_char_t* base = smem + c * S::kSlot;
+      const int qa = qt0 + 32 * it;
+      floatx16 sacc;
+      read_rowc(base, S::offLse, sacc);
+      chain(base + S::offQT, kb, sacc);
+      half8 pf[2];
+      auto softmax = [&](bool masked) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float pv = __builtin_amdgcn_exp2f(sacc[i]);
+          if (POL == 1 && masked) {
+            const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
+            pv = ((unsigned)(q - qlo) < (unsigned)qspan) ? pv : 0.f;
+          }
+          if (POL == 2 && masked) {
+            const int q = qa + 16 * (i >> 3) + 8 * h + (i & 7);
+            pv = (q < nq && check_orders_bf(a.rule, seq_order(a.rule.q, a.rule, min(q, nq - 1)), ko)) ? pv : 0.f;
+          }
+          pf[i >> 3][i & 7] = (_Float16)pv;
+        }
+      };
+      if (POL != 0 && cls == 1) {
+        asm volatile("; edge tile" ::: );
+        softmax(true);
+      } else {
+        asm volatile("; interior tile" ::: );
+        softmax(false);
+      }
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) *reinterpret_cast<lds_half8_t*>(smem + poff(c % 2, s_)) = pf[s_];
+    };
+    for (int it = 0; it < nsteps; it += 4) {
+      astep(IC<0>{}, it);
+      astep(IC<1>{}, it + 1);
+      astep(IC<2>{}, it + 2);
+      astep(IC<3>{}, it + 3);
+    }
+    return;
+  }
+  if (role == 1) {
+    // ================= B: dP, dS of the tile before
+    half8 vb[D / 16];
+    resident(1, vb);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    stage0(IC<1>{});
+    auto bstep = [&](auto C_, int it) __attribute__((always_inline)) {
+      constexpr int c = decltype(C_)::value;
+      stage(C_, IC<1>{}, it);
+      if (tcls(it - 1) == 0) return;
+      const lds_char_t* base = smem + ((c + 3) % 4) * S::kSlot;
+      floatx16 pacc;
+      read_rowc(base, S::offD, pacc);
+      chain(base + S::offOT, vb, pacc);
+      half8 pf[2], sf[2];
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) pf[s_] = read_b128(smem + poff((c + 1) % 2, s_));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sf[i >> 3][i & 7] = (_Float16)((float)pf[i >> 3][i & 7] * pacc[i]);
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) *reinterpret_cast<lds_half8_t*>(smem + soff((c + 1) % 2, s_)) = sf[s_];
+    };
+    for (int it = 0; it < nsteps; it += 4) {
+      bstep(IC<0>{}, it);
+      bstep(IC<1>{}, it + 1);
+      bstep(IC<2>{}, it + 2);
+      bstep(IC<3>{}, it + 3);
+    }
+    return;
+  }
+
+  // ================= C (dV += dO·P, the tile before) or Dk (dK += Q·dS, two before): one code path
+  // each (a runtime role test inside the step spilled ~600 VGPRs)
+  auto accumulate = [&](auto ISC_) __attribute__((always_inline)) {
+    constexpr bool isC = decltype(ISC_)::value;
+    stage0(IC<isC ? 2 : 3>{});
+    floatx16 acc[D / 32];
+#pragma unroll
+    for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[u][i] = 0.f;
+    auto cstep = [&](auto C_, int it) __attribute__((always_inline)) {
+      constexpr int c = decltype(C_)::value;
+      stage(C_, IC<isC ? 2 : 3>{}, it);
+      if constexpr (isC) {
+        if (tcls(it - 1) == 0) return;
+        half8 pf[2];
+#pragma unroll
+        for (int s_ = 0; s_ < 2; ++s_) pf[s_] = read_b128(smem + poff((c + 1) % 2, s_));
+        accum(smem + ((c + 3) % 4) * S::kSlot + S::offOT, pf, acc);
+      } else {
+        if (tcls(it - 2) == 0) return;
+        half8 sf[2];
+#pragma unroll
+        for (int s_ = 0; s_ < 2; ++s_) sf[s_] = read_b128(smem + soff(c % 2, s_));
+        accum(smem + ((c + 2) % 4) * S::kSlot + S::offQT, sf, acc);
+      }
+    };
+    for (int it = 0; it < nsteps; it += 4) {
+      cstep(IC<0>{}, it);
+      cstep(IC<1>{}, it + 1);
+      cstep(IC<2>{}, it + 2);
+      cstep(IC<3>{}, it + 3);
+    }
+    // ---- dV, or dK = scale·Σ dS·Q: rows c = 32u + (i&3) + 8(i>>2) + 4h, column = this lane's key
+    if (!wave_active || key >= nk) return;
+    __half* X = static_cast<__half*>(isC ? a.dV : a.dK) + bi * (int64_t)(isC ? vd : d) * nk;
+    const int dx = isC ? vd : d;
+    const float sc = isC ? 1.f : (float)a.scale;
+    if (dx == D) {
+      const __amdgpu_buffer_rsrc_t xrs = make_rsrc(X, 2u * D * nk);
+      const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nk + (uint32_t)key);
+#pragma unroll
+      for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t so = 2u * (32u * u + (i & 3) + 8u * (i >> 2)) * (uint32_t)nk;
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(acc[u][i] * sc)), xrs, vlane, so,
+                                                0);
+        }
+      return;
+    }
+#pragma unroll
+    for (int u = 0; u < D / 32; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int cc = 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (cc < dx) X[(int64_t)cc * nk + key] = __float2half(acc[u][i] * sc);
+      }
+  };
+  if (role == 2) accumulate(IC<1>{});
+  else accumulate(IC<0>{});
+}
+
 
 // ---------------------------------------------------------------------------
 template <int D, int NW>
@@ -1509,16 +1896,28 @@ hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
 
 // 128 < max(d, v_d) <= 256 (16-B aligned tensors, lengths multiples of 8): both one-wave passes at D =
 // 256, each workgroup on one of two 128-channel output chunks
-template <bool RA = false>
+// OC = 0: the four-role dK / dV pass; OC > 0: the one-wave pass on OC output-channel chunks
+template <int OC = 0, int OCQ = 2>
 hipError_t launch_bwd_wide(const BwdArgs& a, hipStream_t s) {
-  constexpr int D = 256, NW = 4, OC = 2;
+  constexpr int D = 256, NW = 4;
   const int pol = bwd_pol(a.rule);
-  {
+  if constexpr (OC == 0) {  // the four-role pass: S / dP formed once per pair
+    using S = W4Smem;
+    const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
+    const BwdKernel kern = pol == 0   ? bwd_dkdv_w4_kernel<0, true>
+                           : pol == 1 ? bwd_dkdv_w4_kernel<1, true>
+                                      : bwd_dkdv_w4_kernel<2, true>;
+    hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(512), S::kTotal, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  } else {
     using S = DkdvSmem<D, NW>;
     const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
-    const BwdKernel kern = pol == 0   ? bwd_dkdv_kernel<D, NW, 1, 0, true, OC, RA>
-                           : pol == 1 ? bwd_dkdv_kernel<D, NW, 1, 1, true, OC, RA>
-                                      : bwd_dkdv_kernel<D, NW, 1, 2, true, OC, RA>;
+    const BwdKernel kern = pol == 0   ? bwd_dkdv_kernel<D, NW, 1, 0, true, OC>
+                           : pol == 1 ? bwd_dkdv_kernel<D, NW, 1, 1, true, OC>
+                                      : bwd_dkdv_kernel<D, NW, 1, 2, true, OC>;
     hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb * OC)), dim3(NW * 64), S::kTotal, s, a);
@@ -1527,12 +1926,12 @@ hipError_t launch_bwd_wide(const BwdArgs& a, hipStream_t s) {
   }
   using S = DqSmem<D, NW>;
   const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
-  const BwdKernel kern = pol == 0   ? bwd_dq_kernel<D, NW, 1, 0, true, false, false, OC, true>
-                         : pol == 1 ? bwd_dq_kernel<D, NW, 1, 1, true, false, false, OC, true>
-                                    : bwd_dq_kernel<D, NW, 1, 2, true, false, false, OC, true>;
+  const BwdKernel kern = pol == 0   ? bwd_dq_kernel<D, NW, 1, 0, true, false, false, OCQ, true>
+                         : pol == 1 ? bwd_dq_kernel<D, NW, 1, 1, true, false, false, OCQ, true>
+                                    : bwd_dq_kernel<D, NW, 1, 2, true, false, false, OCQ, true>;
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb * OC)), dim3(NW * 64), S::kTotal, s, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb * OCQ)), dim3(NW * 64), S::kTotal, s, a);
   return hipGetLastError();
 }
 
@@ -1572,9 +1971,8 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
 #ifdef FA_DIAG
-  // FA_BWD_VARIANT=1420: the D = 256 dK/dV pass with its operand reads two MFMA pairs ahead (w256b
-  // backward 30.5 against 29.5 ms in one process, so not the default)
-  if (max(a.d, a.v_d) > 128 && diag_variant("FA_BWD_VARIANT") == 1420) return launch_bwd_wide<true>(a, s);
+  // FA_BWD_VARIANT=1421: round 4's D = 256 dK/dV pass (two 128-channel chunks, S / dP formed in each)
+  if (max(a.d, a.v_d) > 128 && diag_variant("FA_BWD_VARIANT") == 1421) return launch_bwd_wide<2, 2>(a, s);
 #endif
   if (max(a.d, a.v_d) > 128) return launch_bwd_wide(a, s);
 #ifdef FA_DIAG
