@@ -1156,6 +1156,359 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_w4_kernel(BwdArgs a) {
 
 
 // ---------------------------------------------------------------------------
+// dQ at D = 256 without the recomputed products: the four-role split of bwd_dkdv_w4_kernel applied to
+// the query-outer pass, a 32-query slice per role set
+//   E  (Sᵀ):  Sᵀ = Kᵀ·Q' (C = -lse2), P = exp2(Sᵀ) (masked)          -> P   hand-over
+//   F  (dPᵀ): dPᵀ = Vᵀ·dO (C = -D) of the tile before, dSᵀ = P∘dPᵀ    -> dSᵀ hand-over
+//   G0, G1:   dQ += K·dSᵀ of the tile two before, channels 0-127 / 128-255
+// (the one-wave pass with OC = 2 formed Sᵀ and dPᵀ in both channel chunks: 80 MFMAs a 32 x 32 pair,
+// this pass 48).  Waves 0-3 = E0, F0, E1, F1 and 4-7 = G0/0, G1/0, G0/1, G1/1: every SIMD pairs a
+// 16-MFMA role with an 8-MFMA one.  Key tiles of 32 ([D][32] images like the dK/dV pass's query tiles).
+struct W4DqSmem {
+  static constexpr int D = 256;
+  static constexpr int kBM = 64;              // queries per workgroup: two slices of 32
+  static constexpr int kRow = D * kBM * 2;    // Q (or dO) row image (prologue only): 32 KB
+  static constexpr int kKT = D * 64;          // one [D][32] K16 image: 16 KB
+  static constexpr int offKT = 0, offVT = kKT;
+  static constexpr int kSlot = 2 * kKT;
+  static constexpr int kNS = 4;               // key-tile ring
+  static constexpr int kXW = 2048;            // one slice's P (or dSᵀ) of a tile, lane-linear
+  static constexpr int offP = kNS * kSlot;
+  static constexpr int offS = offP + 4 * kXW;
+  static constexpr int kUsed = offS + 4 * kXW;
+  static constexpr int kTotal = kUsed > 2 * kRow ? kUsed : 2 * kRow;
+};
+
+template <int POL, bool ALN>
+__global__ __launch_bounds__(512, 1) void bwd_dq_w4_kernel(BwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char_t* smem = (lds_char_t*)smem_raw;
+  using S = W4DqSmem;
+  constexpr int D = S::D;
+  constexpr int kThr = 512;
+  constexpr int kBM = S::kBM;
+  constexpr int kKChunks = D * 4;                 // 16-B chunks of one [D][32] tile
+  constexpr int kCPT = 2 * kKChunks / kThr;       // K and V chunks per thread
+  constexpr float kNegInf = -__builtin_huge_valf();
+  const int nq = a.rule.q.n, nk = a.rule.k.n;
+  const uint32_t nqb = (nq + kBM - 1) / kBM;
+  const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t bi = bid / nqb;
+  const int q0 = (int)(nqb - 1 - (bid % nqb)) * kBM;  // latest (heaviest under causal) blocks first
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sl = (w >> 1) & 1;                    // query slice
+  const int role = (w & 1) + 2 * (w >> 2);        // 0 E, 1 F, 2 G0, 3 G1
+  const int h = lane >> 5, r = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const int sig = ((tp & 1) << 1) | (tp >> 1);
+  const float c2 = (float)a.scale * kLog2e;
+  const int d = a.d, vd = a.v_d;
+  const __half* Q = static_cast<const __half*>(a.Q) + bi * (int64_t)d * nq;
+  const __half* dO = static_cast<const __half*>(a.dO) + bi * (int64_t)vd * nq;
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(static_cast<const __half*>(a.K) + bi * (int64_t)d * nk, 2u * d * nk);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(static_cast<const __half*>(a.V) + bi * (int64_t)vd * nk, 2u * vd * nk);
+  const int wq0 = q0 + 32 * sl;
+  const int qi = wq0 + r;
+  const bool wave_active = wq0 < nq;
+
+  // ---- Q, dO blocks into LDS (every thread, 128-B rows); roles E / F read their resident operands
+  {
+    constexpr int kRPT = 2 * D * (kBM / 8) / kThr, kHalf = D * (kBM / 8) / kThr;
+    static_assert(kHalf * kThr == D * (kBM / 8), "resident chunks must divide over the workgroup");
+    const __amdgpu_buffer_rsrc_t qrs2 = make_rsrc(Q, 2u * d * nq), ors2 = make_rsrc(dO, 2u * vd * nq);
+    u32x4 rv[kRPT];
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
+      const int c = j / (kBM / 8), m = j % (kBM / 8);
+      const bool in = c < (which ? vd : d) && q0 + 8 * m < nq;
+      if constexpr (ALN)
+        rv[jj] = __builtin_amdgcn_raw_buffer_load_b128(which ? ors2 : qrs2,
+                                                       in ? (uint32_t)c * (uint32_t)nq * 2u + 16u * m : 0x80000000u, 2 * q0, 0);
+      else
+        rv[jj] = buf_load8h(which ? ors2 : qrs2, (uint32_t)c * (uint32_t)nq * 2u, q0 + 8 * m, nq, c < (which ? vd : d));
+    }
+#pragma unroll
+    for (int jj = 0; jj < kRPT; ++jj) {
+      const int which = jj >= kHalf, j = tid + kThr * (jj - which * kHalf);
+      const int c = j / (kBM / 8), m = j % (kBM / 8);
+      *reinterpret_cast<lds_u32x4_t*>(smem + which * S::kRow + c * (2 * kBM) + m * 16) = rv[jj];
+    }
+  }
+  __syncthreads();
+
+  // ---- key range of this query block, per-lane / per-wave key intervals of the slice's queries
+  const int qlast = min(q0 + kBM, nq) - 1;
+  int kb = 0, ke = nk;
+  if (POL != 0) k_range_for_q_block(a.rule, q0, qlast, &kb, &ke);
+  const int kt0 = (kb / 32) * 32;
+  const int ntiles = (ke > kb) ? (ke - kt0 + 31) / 32 : 0;
+  int klo = 0, kspan = nk, wlo_min = 0, wlo_max = 0, whi_min = nk - 1, whi_max = nk - 1;
+  if (POL == 1 && wave_active) {
+    int khi;
+    key_interval(a.rule, min(qi, nq - 1), &klo, &khi);
+    kspan = max(khi - klo + 1, 0);
+    const int last = min(31, nq - 1 - wq0);
+    wlo_min = __builtin_amdgcn_readfirstlane(klo);
+    whi_min = __builtin_amdgcn_readfirstlane(khi);
+    wlo_max = __builtin_amdgcn_readlane(klo, last);
+    whi_max = __builtin_amdgcn_readlane(khi, last);
+  }
+  // class of tile t for this slice (0 outside [0, ntiles))
+  auto tcls = [&](int t) -> int {
+    if (t < 0 || t >= ntiles || !wave_active) return 0;
+    const int ka = kt0 + 32 * t, kz = ka + 31;
+    if (POL == 0) return kz < nk ? 2 : 1;
+    if (POL == 2) {  // class 2 only for tiles wholly inside nk (the staged tail past nk is masked)
+      if (ka >= nk) return 0;
+      const int c = tile_class(a.rule, wq0, min(wq0 + 31, nq - 1), ka, min(kz, nk - 1));
+      return (c == 2 && kz >= nk) ? 1 : c;
+    }
+    if (wlo_min > kz || whi_max < ka) return 0;
+    return (wlo_max <= ka && whi_min >= kz && kz < nk) ? 2 : 1;
+  };
+
+  // ---- key-tile staging, every thread (K, V chunks: 8 keys of one channel row)
+  uint32_t voff[kCPT];
+  int crow_[kCPT], cm_[kCPT];
+#pragma unroll
+  for (int j = 0; j < kCPT; ++j) {
+    const int idx = (tid + kThr * j) % kKChunks;
+    crow_[j] = idx >> 2;
+    cm_[j] = idx & 3;
+    voff[j] = (uint32_t)crow_[j] * (uint32_t)nk * 2u + (ALN ? 16u * cm_[j] : 0u);
+  }
+  u32x4 kr[2][kCPT];
+  auto is_v = [&](int j) -> bool { return j >= kKChunks / kThr; };
+  auto load_tile = [&](int ka, int set) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isV = is_v(j);
+      if constexpr (ALN) {
+        const bool out = ka + 8 * cm_[j] >= nk || crow_[j] >= (isV ? vd : d);
+        kr[set][j] = buf_load16(isV ? vrs : krs, voff[j], 2 * min(ka, nk), out);
+      } else {
+        kr[set][j] = buf_load8h(isV ? vrs : krs, voff[j], ka + 8 * cm_[j], nk, crow_[j] < (isV ? vd : d));
+      }
+    }
+  };
+  auto store_tile = [&](int slot, int set) __attribute__((always_inline)) {
+    lds_char_t* base = smem + slot * S::kSlot;
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+      const bool isV = is_v(j);
+      *reinterpret_cast<lds_u32x4_t*>(base + (isV ? S::offVT : S::offKT) + q16_off(crow_[j], cm_[j])) = kr[set][j];
+    }
+  };
+  auto poff = [&](int xs, int j) -> uint32_t { return S::offP + (2 * xs + sl) * S::kXW + j * 1024 + lane * 16; };
+  auto soff = [&](int xs, int j) -> uint32_t { return S::offS + (2 * xs + sl) * S::kXW + j * 1024 + lane * 16; };
+
+  // Steps it = 0 .. ntiles + 1: E handles tile it, F tile it-1, G0 / G1 tile it-2 (as the dK/dV pass)
+  const int nsteps = ntiles + 2;
+  // (TAG: one marker per role, see bwd_dkdv_w4_kernel)
+  auto stage = [&](auto C_, auto TAG_, int it) __attribute__((always_inline)) {
+    constexpr int c = decltype(C_)::value;
+    asm volatile("; stage, role %0" ::"i"(decltype(TAG_)::value));
+    __syncthreads();
+    store_tile((c + 1) % 4, (c + 1) % 2);
+    load_tile(kt0 + 32 * (it + 3), (c + 1) % 2);
+  };
+  load_tile(kt0, 0);
+  auto stage0 = [&](auto TAG_) __attribute__((always_inline)) {
+    asm volatile("; stage 0, role %0" ::"i"(decltype(TAG_)::value));
+    __syncthreads();  // the Q / dO images are retired
+    store_tile(0, 0);
+    load_tile(kt0 + 32, 1);
+    load_tile(kt0 + 64, 0);
+  };
+  auto read_op = [&](const lds_char_t* img, int s_) __attribute__((always_inline)) -> half8 {
+    half8 x;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const uint32_t off = q16_off(16 * s_ + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
+      const half4 t = tr_read(img + off);
+      if (e == 0) x.lo = t; else x.hi = t;
+    }
+    return x;
+  };
+  auto resident = [&](int which, half8 (&xb)[D / 16]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s_ = 0; s_ < D / 16; ++s_)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int crow = 16 * s_ + 8 * (g >> 1) + 4 * e + tq;
+        const int col = 32 * sl + 16 * (g & 1) + 4 * tp;
+        const half4 x = tr_read(smem + which * S::kRow + crow * (2 * kBM) + col * 2);
+        if (e == 0) xb[s_].lo = x; else xb[s_].hi = x;
+      }
+  };
+  auto rowconst = [&](const void* ws, float dflt) -> floatx16 {
+    const float* p = static_cast<const float*>(ws) + bi * (int64_t)nq;
+    const float v = (qi < nq) ? p[qi] : dflt;
+    floatx16 x;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = v;
+    return x;
+  };
+  auto chain = [&](const lds_char_t* img, const half8 (&xb)[D / 16], floatx16 acc) __attribute__((always_inline)) -> floatx16 {
+    constexpr int kS = D / 16, kAh = 2;
+    half8 a8[kAh + 1];
+#pragma unroll
+    for (int s_ = 0; s_ < kAh; ++s_) a8[s_] = read_op(img, s_);
+#pragma unroll
+    for (int s_ = 0; s_ < kS; ++s_) {
+      if (s_ + kAh < kS) a8[(s_ + kAh) % (kAh + 1)] = read_op(img, s_ + kAh);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8[s_ % (kAh + 1)], xb[s_], acc, 0, 0, 0);
+    }
+    return acc;
+  };
+
+  if (role == 0) {
+    // ================= E: Sᵀ, P
+    half8 qf[D / 16];
+    resident(0, qf);
+#pragma unroll
+    for (int s_ = 0; s_ < D / 16; ++s_) qf[s_] = scale8(qf[s_], c2);
+    const floatx16 negl = rowconst(a.ws_lse, kNegInf);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    stage0(IC<0>{});
+    const int qo = (POL == 2) ? seq_order(a.rule.q, a.rule, min(qi, nq - 1)) : 0;
+    auto estep = [&](auto C_, int it) __attribute__((always_inline)) {
+      constexpr int c = decltype(C_)::value;
+      stage(C_, IC<0>{}, it);
+      const int cls = tcls(it);
+      if (cls == 0) return;
+      const lds_char_t* base = smem + c * S::kSlot;
+      const int ka = kt0 + 32 * it;
+      const floatx16 sacc = chain(base + S::offKT, qf, negl);
+      half8 pf[2];
+      auto softmax = [&](bool masked) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float pv = __builtin_amdgcn_exp2f(sacc[i]);
+          if (masked) {
+            const int kk = ka + 16 * (i >> 3) + 8 * h + (i & 7);
+            const bool ok = (POL == 1)   ? ((unsigned)(kk - klo) < (unsigned)kspan)
+                            : (POL == 2) ? (kk < nk && check_orders_bf(a.rule, qo, seq_order(a.rule.k, a.rule, min(kk, nk - 1))))
+                                         : (kk < nk);
+            pv = ok ? pv : 0.f;
+          }
+          pf[i >> 3][i & 7] = (_Float16)pv;
+        }
+      };
+      if (cls == 1) {
+        asm volatile("; edge tile" ::: );
+        softmax(true);
+      } else {
+        asm volatile("; interior tile" ::: );
+        softmax(false);
+      }
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) *reinterpret_cast<lds_half8_t*>(smem + poff(c % 2, s_)) = pf[s_];
+    };
+    for (int it = 0; it < nsteps; it += 4) {
+      estep(IC<0>{}, it);
+      estep(IC<1>{}, it + 1);
+      estep(IC<2>{}, it + 2);
+      estep(IC<3>{}, it + 3);
+    }
+    return;
+  }
+  if (role == 1) {
+    // ================= F: dPᵀ, dSᵀ of the tile before
+    half8 of[D / 16];
+    resident(1, of);
+    const floatx16 negd = rowconst(a.ws_D, 0.f);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    stage0(IC<1>{});
+    auto fstep = [&](auto C_, int it) __attribute__((always_inline)) {
+      constexpr int c = decltype(C_)::value;
+      stage(C_, IC<1>{}, it);
+      if (tcls(it - 1) == 0) return;
+      const lds_char_t* base = smem + ((c + 3) % 4) * S::kSlot;
+      const floatx16 pacc = chain(base + S::offVT, of, negd);
+      half8 pf[2], sf[2];
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) pf[s_] = read_b128(smem + poff((c + 1) % 2, s_));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sf[i >> 3][i & 7] = (_Float16)((float)pf[i >> 3][i & 7] * pacc[i]);
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) *reinterpret_cast<lds_half8_t*>(smem + soff((c + 1) % 2, s_)) = sf[s_];
+    };
+    for (int it = 0; it < nsteps; it += 4) {
+      fstep(IC<0>{}, it);
+      fstep(IC<1>{}, it + 1);
+      fstep(IC<2>{}, it + 2);
+      fstep(IC<3>{}, it + 3);
+    }
+    return;
+  }
+
+  // ================= G0 / G1: dQ += K·dSᵀ (tile two before), one channel half each
+  auto accumulate = [&](auto HH_) __attribute__((always_inline)) {
+    constexpr int hh = decltype(HH_)::value;
+    constexpr int kU = D / 64;  // 32-channel blocks of the half
+    stage0(IC<2 + hh>{});
+    floatx16 dq[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dq[u][i] = 0.f;
+    auto gstep = [&](auto C_, int it) __attribute__((always_inline)) {
+      constexpr int c = decltype(C_)::value;
+      stage(C_, IC<2 + hh>{}, it);
+      if (tcls(it - 2) == 0) return;
+      half8 sf[2];
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) sf[s_] = read_b128(smem + soff(c % 2, s_));
+      const lds_char_t* img = smem + ((c + 2) % 4) * S::kSlot + S::offKT;
+      constexpr int kN = 2 * kU, kAh = 2;
+      half8 y[kAh + 1];
+      auto rd = [&](int n) __attribute__((always_inline)) {
+        y[n % (kAh + 1)] = read_b128(img + q16_off(32 * (kU * hh + n % kU) + r, 2 * (n / kU) + h));
+      };
+#pragma unroll
+      for (int n = 0; n < kAh; ++n) rd(n);
+#pragma unroll
+      for (int n = 0; n < kN; ++n) {
+        if (n + kAh < kN) rd(n + kAh);
+        dq[n % kU] = __builtin_amdgcn_mfma_f32_32x32x16_f16(y[n % (kAh + 1)], sf[n / kU], dq[n % kU], 0, 0, 0);
+      }
+    };
+    for (int it = 0; it < nsteps; it += 4) {
+      gstep(IC<0>{}, it);
+      gstep(IC<1>{}, it + 1);
+      gstep(IC<2>{}, it + 2);
+      gstep(IC<3>{}, it + 3);
+    }
+    if (!wave_active || qi >= nq) return;
+    __half* dQ = static_cast<__half*>(a.dQ) + bi * (int64_t)d * nq;
+    const float sc = (float)a.scale;
+    if (d == D) {
+      const __amdgpu_buffer_rsrc_t qrs_ = make_rsrc(dQ, 2u * d * nq);
+      const uint32_t vlane = 2u * ((uint32_t)(4 * h) * (uint32_t)nq + (uint32_t)qi);
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(dq[u][i] * sc)), qrs_, vlane,
+                                                2u * (32u * (kU * hh + u) + (i & 3) + 8u * (i >> 2)) * (uint32_t)nq, 0);
+      return;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int cc = 32 * (kU * hh + u) + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (cc < d) dQ[(int64_t)cc * nq + qi] = __float2half(dq[u][i] * sc);
+      }
+  };
+  if (role == 2) accumulate(IC<0>{});
+  else accumulate(IC<1>{});
+}
+
+// ---------------------------------------------------------------------------
 template <int D, int NW>
 struct DqSmem {
   static constexpr int kBM = 32 * NW;                 // queries per workgroup
@@ -1896,8 +2249,9 @@ hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
 
 // 128 < max(d, v_d) <= 256 (16-B aligned tensors, lengths multiples of 8): both one-wave passes at D =
 // 256, each workgroup on one of two 128-channel output chunks
-// OC = 0: the four-role dK / dV pass; OC > 0: the one-wave pass on OC output-channel chunks
-template <int OC = 0, int OCQ = 2>
+// OC / OCQ = 0: the four-role dK / dV / dQ passes; > 0: the one-wave passes on that many output-channel
+// chunks (round 4's structure, FA_BWD_VARIANT=1421)
+template <int OC = 0, int OCQ = 0>
 hipError_t launch_bwd_wide(const BwdArgs& a, hipStream_t s) {
   constexpr int D = 256, NW = 4;
   const int pol = bwd_pol(a.rule);
@@ -1924,15 +2278,27 @@ hipError_t launch_bwd_wide(const BwdArgs& a, hipStream_t s) {
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  using S = DqSmem<D, NW>;
-  const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
-  const BwdKernel kern = pol == 0   ? bwd_dq_kernel<D, NW, 1, 0, true, false, false, OCQ, true>
-                         : pol == 1 ? bwd_dq_kernel<D, NW, 1, 1, true, false, false, OCQ, true>
-                                    : bwd_dq_kernel<D, NW, 1, 2, true, false, false, OCQ, true>;
-  hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb * OCQ)), dim3(NW * 64), S::kTotal, s, a);
-  return hipGetLastError();
+  if constexpr (OCQ == 0) {  // the four-role pass: Sᵀ / dPᵀ formed once per pair
+    using S = W4DqSmem;
+    const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
+    const BwdKernel kern = pol == 0   ? bwd_dq_w4_kernel<0, true>
+                           : pol == 1 ? bwd_dq_w4_kernel<1, true>
+                                      : bwd_dq_w4_kernel<2, true>;
+    hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(512), S::kTotal, s, a);
+    return hipGetLastError();
+  } else {
+    using S = DqSmem<D, NW>;
+    const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
+    const BwdKernel kern = pol == 0   ? bwd_dq_kernel<D, NW, 1, 0, true, false, false, OCQ, true>
+                           : pol == 1 ? bwd_dq_kernel<D, NW, 1, 1, true, false, false, OCQ, true>
+                                      : bwd_dq_kernel<D, NW, 1, 2, true, false, false, OCQ, true>;
+    hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb * OCQ)), dim3(NW * 64), S::kTotal, s, a);
+    return hipGetLastError();
+  }
 }
 
 template <int D>
