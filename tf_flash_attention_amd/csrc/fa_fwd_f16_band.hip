@@ -8,12 +8,13 @@
 // list of blocks ("items": the query blocks of consecutive (batch, head) slices in order)
 // as ONE stream of key tiles:
 //
-//   * every item is exactly T positions (T + 2 a multiple of 4, 10 <= T <= 22); group 1 (queries
-//     128-255) works two key tiles ahead of group 0, so an item streams T + 2 tiles (a ws = 256
-//     band: 10 positions for 12 tiles).  Positions past an item's band load zeros and are skipped
-//     by every wave.  The item loop is unrolled over its T positions, so ring slots, staging
-//     registers and every per-position decision are compile-time;
-//   * the K/V staging (registers, loaded one position ahead of their LDS store, 1.2 tiles a
+//   * every item is exactly T positions (T + 3 a multiple of 4, 9 <= T <= 21); wave pair o (the
+//     item's queries 64o .. 64o+63) works o key tiles ahead of pair 0, so an item streams T + 3
+//     tiles (a ws = 256 band: 9 positions for 12 tiles, each pair inside its own band at every
+//     position).  Positions past an item's band load zeros and are skipped by every wave.  The
+//     item loop is unrolled over its T positions, so ring slots, staging registers and every
+//     per-position decision are compile-time;
+//   * the K/V staging (registers, loaded one position ahead of their LDS store, 1.33 tiles a
 //     position; LDS rings of four slots) runs straight across item boundaries;
 //   * the next item's Q image is loaded one 16-B chunk per thread at positions 2-5 and stored
 //     into the second of two LDS Q buffers one position later (3-6); each wave reads its new Q
@@ -64,48 +65,49 @@ constexpr int kOffV = kOffK + kNS * kTile;
 constexpr int kOffLM = kOffV + kNS * kTile;   // l (fp32) and m (fp16) of a finished item: 1.5 KB
 constexpr int kOffTab = kOffLM + 6 * kBM;     // kt0 of every query block of a slice (int32)
 constexpr int kMaxTab = 4096;                 // query blocks per slice: nq <= 1M
-constexpr int kSmem = kOffTab + 4 * kMaxTab;  // 145.5 KB
+constexpr int kOffDummy = kOffTab + 4 * kMaxTab;  // scratch chunk per thread for the padding stores
+constexpr int kSmem = kOffDummy + 16 * kNW * 64;  // 153.5 KB
 // Item timeline (positions it = 0 .. T-1 of item n+1): MFMA(0) writes item n's l / m (and group
 // 1's O) into LDS, MFMA(1) group 0's O (O over Q buffer n&1, dead by then); MFMA(2), MFMA(3) store
 // it to HBM; MFMA(2..5) load item n+2's Q chunks, MFMA(3..6) store them into buffer n&1 (after the
-// O reads); VALU(T-1) reads them as fragments: with T >= 10 a barrier separates every store from
+// O reads); VALU(T-1) reads them as fragments: with T >= 9 a barrier separates every store from
 // every read.
-constexpr int kMinT = 10;
-constexpr int kMaxT = 22;
-// staggered staging schedule (T positions, NT = T + 2 tiles an item, rings of four slots: tile j in
-// slot j & 3).  Tile j of an item is read by group 0 as K at position j (j < T) and as V at j + 1, by
-// group 1 as K at j - 2 and as V at j - 1 (j >= 2).  A group's chunk of a tile is stored in its MFMA
-// phase of position p (interval 2p + g), visible two intervals later, and only after every read of
-// the slot's previous tile (j - 4).  Entry i (0, 1) of the tiles group g stores at position p;
-// indices >= NT are the next item's tile index - NT; -1 none.  A group with one tile where the
-// other has two repeats it (the same chunk to the same place: the pair runs branch-free).
-__host__ __device__ constexpr int stag_k1(int T, int p, int g, int i) {
-  const int NT = T + 2;
-  if (g == 0) {
-    if (p == 0) return i == 0 ? 1 : 3;
-    if (p <= T - 2) return p + 3;
-    return i == 0 ? NT : NT + 2;
-  }
-  if (p == 0) return 3;
-  if (p <= T - 3) return p + 3;
-  if (p == T - 2) return i == 0 ? T + 1 : NT;
-  return i == 0 ? NT + 1 : NT + 2;
+constexpr int kMinT = 9;
+constexpr int kMaxT = 21;
+// Staggered wave pairs (T positions, NT = T + 3 tiles an item, rings of four slots: tile j of the
+// stream in slot j & 3).  Wave pair o (waves 2o and 2o + 1, the item's queries 64o .. 64o + 63; o =
+// 2·grp + ((w >> 1) & 1)) works on tile p + o at position p, so each pair spans only the tiles of its
+// own 64 queries (a ws = 256 band: 9 positions for 12 tiles, where one offset per group of four waves
+// needed 10 and every wave spent one of them outside its band).  K of tile j is read by pair o at
+// position j - o (interval 2p + (o >> 1)), V of tile j at position j - o + 1 (the PV of the position
+// before).  A chunk stored in a group's MFMA phase (interval I) is published by the lgkmcnt(0) before
+// that phase's barrier, so it is readable from interval I + 1, and it may be stored only after the last
+// read of the slot's previous tile (j - 4).  Each interior tile then has two intervals, one per group,
+// and each group stores its own threads' chunks: K(p+3) and V(p+2) by group 0, K(p+4) and V(p+3) by
+// group 1 at position p.  The item boundary has one: group 1 stores the next item's K(0), K(1) whole at
+// position T-1 and V(0), V(1) whole at position 0, group 0 K(2), K(3) whole at 0 and V(2), V(3) whole at
+// 1 ("whole": its own chunk and the other group's, channel rows 32 apart).
+// Entry i of the chunks group g stores at position p: the tile j relative to the item (T + 3 + j: the
+// next item's j; -1: the previous item's T + 2) and the part (0 the thread's own chunk, 1 the other
+// group's).  kStDummy: no tile (the entry loads zeros and stores them to a scratch chunk, so every
+// position issues a fixed set of vector-memory operations and hipcc's vmcnt waits stay exact).
+constexpr int kStDummy = -1000;
+__host__ __device__ constexpr int stk_n(int T, int p) { return (p == 0 || p == T - 1) ? 4 : 1; }
+__host__ __device__ constexpr int stk_j(int T, int p, int g, int i) {
+  if (g == 0) return p == 0 ? (i < 2 ? 2 : 3) : (i == 0 ? p + 3 : kStDummy);
+  return p == T - 1 ? (i < 2 ? T + 3 : T + 4) : (i == 0 ? p + 4 : kStDummy);
 }
-__host__ __device__ constexpr int stag_v1(int T, int p, int g, int i) {
-  const int NT = T + 2;
-  if (g == 0) {
-    if (p == 0) return i == 0 ? 0 : 2;
-    if (p == 1) return i == 0 ? 1 : 3;
-    return p + 2;
-  }
-  if (p == 0) return i == 0 ? 1 : 2;
-  if (p == 1) return 3;
-  if (p <= T - 2) return p + 2;
-  return i == 0 ? T + 1 : NT;
+__host__ __device__ constexpr int stk_part(int T, int p, int g, int i) {
+  return ((g == 0 && p == 0) || (g == 1 && p == T - 1)) ? (i & 1) : 0;
 }
-// tiles (per group) stored at position p: two at the item boundary, one elsewhere
-__host__ __device__ constexpr int stag_nk(int T, int p) { return (p == 0 || p >= T - 2) ? 2 : 1; }
-__host__ __device__ constexpr int stag_nv(int T, int p) { return (p <= 1 || p == T - 1) ? 2 : 1; }
+__host__ __device__ constexpr int stv_n(int, int p) { return p <= 1 ? 4 : 1; }
+__host__ __device__ constexpr int stv_j(int, int p, int g, int i) {
+  if (g == 0) return p == 0 ? (i == 0 ? -1 : kStDummy) : p == 1 ? (i < 2 ? 2 : 3) : (i == 0 ? p + 2 : kStDummy);
+  return p == 0 ? (i < 2 ? 0 : 1) : (i == 0 ? p + 3 : kStDummy);
+}
+__host__ __device__ constexpr int stv_part(int, int p, int g, int i) {
+  return ((g == 0 && p == 1) || (g == 1 && p == 0)) ? (i & 1) : 0;
+}
 constexpr float kRescaleThr = 8.f;
 // after a 16-B buffer store: a wait state before any VALU may overwrite its data VGPRs (hipcc,
 // ROCm 7.2, emitted such a write as the very next instruction and the stored dword arrived corrupted:
@@ -145,19 +147,19 @@ struct Item {
   int32_t kt0;  // first key of its first tile (nk past the list: every load reads zeros)
 };
 
-// T (positions per item) is a template parameter, T + 2 a multiple of 4: the item loop is unrolled
+// T (positions per item) is a template parameter, T + 3 a multiple of 4: the item loop is unrolled
 // over its positions, so ring slots, staging registers and every "which position of the item"
-// decision are compile-time (no per-phase selects or dummy operations)
+// decision are compile-time (no per-phase selects)
 template <int T>
 __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) {
-  constexpr int NT = T + 2;  // tiles an item streams
+  constexpr int NT = T + 3;  // tiles an item streams
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
   const FwdArgs& a = ba.a;
   constexpr float kNegInf = -__builtin_huge_valf();
 
   const int nq = a.rule.q.n, nk = a.rule.k.n;
-  static_assert((T + 2) % 4 == 0 && T >= kMinT && T <= kMaxT, "T: T + 2 a multiple of 4, in [kMinT, kMaxT]");
+  static_assert((T + 3) % 4 == 0 && T >= kMinT && T <= kMaxT, "T: T + 3 a multiple of 4, in [kMinT, kMaxT]");
   const int nqb = (nq + kBM - 1) / kBM;
   // this workgroup's items: first + stride * local, inside [it_begin, it_end).
   //   contiguous: a run of consecutive items per workgroup (stride 1);
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = w >> 2;  // waves w and w+4 share a SIMD
-  const int toff = 2 * grp;  // this group's tile at position p is p + toff
+  const int toff = 2 * grp + ((w >> 1) & 1);  // this wave pair's tile at position p is p + toff
   const int h = lane >> 5, r = lane & 31;
   const int gq = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const int d = a.d, vd = a.v_d;
@@ -204,13 +206,12 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   // into LDS, so the stream's item switch is a table read, not two binary searches
   const lds_char_t* tab = smem + kOffTab;
   for (int qb = threadIdx.x; qb < nqb; qb += kNW * 64) {
-    // the first tile group 0 needs, and two before group 1's first (may be < 0)
-    int kb, ke;
-    k_range_for_q_block(a.rule, qb * kBM, min(qb * kBM + kBM / 2, nq) - 1, &kb, &ke);
-    int kt = ke > kb ? (kb / kBN) * kBN : nk;
-    if (qb * kBM + kBM / 2 < nq) {
-      k_range_for_q_block(a.rule, qb * kBM + kBM / 2, min(qb * kBM + kBM, nq) - 1, &kb, &ke);
-      if (ke > kb) kt = min(kt, (kb / kBN) * kBN - 2 * kBN);
+    // the item's first tile: o tiles below wave pair o's first, the lowest over the pairs (may be < 0)
+    int kt = nk;
+    for (int o = 0; o < 4 && qb * kBM + 64 * o < nq; ++o) {
+      int kb, ke;
+      k_range_for_q_block(a.rule, qb * kBM + 64 * o, min(qb * kBM + 64 * o + 64, nq) - 1, &kb, &ke);
+      if (ke > kb) kt = min(kt, (kb / kBN) * kBN - o * kBN);
     }
     *reinterpret_cast<__attribute__((address_space(3))) int*>(smem + kOffTab + 4 * qb) = kt;
   }
@@ -251,6 +252,11 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   const int cm = tid & 7, crow = tid >> 3;
   const uint32_t goff = (uint32_t)crow * (uint32_t)nk * 2u + 16u * cm;
   const uint32_t koff = crow < d ? goff : 0x80000000u, voff = crow < vd ? goff : 0x80000000u;
+  // the other group's chunk of the same 8 keys (channel row crow ^ 32): the whole-tile stores at the
+  // item boundary
+  const int crowp = crow ^ 32;
+  const uint32_t goffp = (uint32_t)crowp * (uint32_t)nk * 2u + 16u * cm;
+  const uint32_t koffp = crowp < d ? goffp : 0x80000000u, voffp = crowp < vd ? goffp : 0x80000000u;
   const uint32_t kwo = crow * 128 + ((cm * 16) ^ ((crow & 2) << 5));
   const uint32_t vwo = crow * 128 + 16 * (cm ^ ((crow >> 1) & 7));
   auto load = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t slb, int k0) -> u32x4 __attribute__((always_inline)) {
@@ -278,30 +284,48 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
                                                  x.sl * qsl + 2 * min(x.q0, nq), 0);
   };
 
-  // ---- prologue: Q(item 0) into Q buffer 0, K(0..2) and V(0) into their ring slots (V slots 1
-  //      and 3 zeroed: the first PV of each group reads them against P = 0); the chunks this
-  //      thread's group stores at position 0 into the staging registers
-  u32x4 kst[2], vst[2];
+  // ---- staging entries (see stk_j / stv_j): the LDS place of entry (j, part) and its load
+  auto st_off = [&](int base, int j, int pt, uint32_t wo) -> int __attribute__((always_inline)) {
+    return j == kStDummy ? kOffDummy + 16 * tid : base + (j & 3) * kTile + (int)(pt ? wo ^ 4096u : wo);
+  };
+  // entry (j0, pt0) of group 0 / (j1, pt1) of group 1 for a store one position on: j relative to the
+  // current item (>= NT: the next item's j - NT); a dummy entry reads zeros (k0 = nk).  One load with
+  // the group's operands selected (scalar selects: a load per group behind a branch costs ~12 SALU)
+  auto st_load = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t offp, uint32_t slsz, int j0, int pt0, int j1,
+                     int pt1) -> u32x4 __attribute__((always_inline)) {
+    const bool d0 = j0 == kStDummy, d1 = j1 == kStDummy, n0 = !d0 && j0 >= NT, n1 = !d1 && j1 >= NT;
+    const int k00 = d0 ? nk : (n0 ? nxt.kt0 + (j0 - NT) * kBN : cur.kt0 + j0 * kBN);
+    const int k01 = d1 ? nk : (n1 ? nxt.kt0 + (j1 - NT) * kBN : cur.kt0 + j1 * kBN);
+    const int sl0 = n0 ? nxt.sl : cur.sl, sl1 = n1 ? nxt.sl : cur.sl;
+    const int k0 = (k00 == k01) ? k00 : (grp ? k01 : k00);
+    const int slb = ((sl0 == sl1) ? sl0 : (grp ? sl1 : sl0)) * (int)slsz;
+    const int pt = (pt0 == pt1) ? pt0 : (grp ? pt1 : pt0);
+    return load(rs, pt ? offp : off, (uint32_t)slb, k0);
+  };
+
+  // ---- prologue: Q(item 0) into Q buffer 0, K(0) and K(1) whole into their ring slots, every V slot
+  //      zeroed (position 0's PVs read them against P = 0); the chunks this thread's group stores at
+  //      position 0 into the staging registers
+  u32x4 kst[4], vst[4];
   {
-    u32x4 kp[3], vp[2], qv[4];
+    u32x4 kp[4], qv[4];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) kp[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + j * kBN);
+    for (int j = 0; j < 4; ++j) kp[j] = load(krs, (j & 1) ? koffp : koff, cur.sl * ksl, cur.kt0 + (j >> 1) * kBN);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) vp[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + j * kBN);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      kst[j] = load(krs, koff, cur.sl * ksl, cur.kt0 + (grp ? stag_k1(T, 0, 1, j) : stag_k1(T, 0, 0, j)) * kBN);
-      vst[j] = load(vrs, voff, cur.sl * vsl, cur.kt0 + (grp ? stag_v1(T, 0, 1, j) : stag_v1(T, 0, 0, j)) * kBN);
+    for (int i = 0; i < 4; ++i) {
+      kst[i] = st_load(krs, koff, koffp, ksl, stk_j(T, 0, 0, i), stk_part(T, 0, 0, i), stk_j(T, 0, 1, i),
+                       stk_part(T, 0, 1, i));
+      vst[i] = st_load(vrs, voff, voffp, vsl, stv_j(T, 0, 0, i), stv_part(T, 0, 0, i), stv_j(T, 0, 1, i),
+                       stv_part(T, 0, 1, i));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) qv[j] = qload(cur, j);
 #pragma unroll
     for (int j = 0; j < 4; ++j) store(ql_lane + j * 16 * kQRow, qv[j]);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) store(kOffK + j * kTile + kwo, kp[j]);
-    store(kOffV + vwo, vp[0]);
-    store(kOffV + kTile + 16 * tid, u32x4{0, 0, 0, 0});
-    store(kOffV + 3 * kTile + 16 * tid, u32x4{0, 0, 0, 0});
+    for (int j = 0; j < 4; ++j) store(kOffK + (j >> 1) * kTile + ((j & 1) ? kwo ^ 4096u : kwo), kp[j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store(kOffV + j * kTile + 16 * tid, u32x4{0, 0, 0, 0});
   }
   __syncthreads();
 
@@ -599,11 +623,11 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     constexpr int it = decltype(IT_)::value;
     constexpr int c = it & 3;
     __builtin_amdgcn_s_setprio(1);
-    // (this group's tiles are p + toff, toff in {0, 2}, tile j in slot j & 3, and (j + toff) & 3 =
-    // ((j & 3) + toff) & 3; the PV at position 0 is of the previous item's tile T-1+toff)
+    // (this pair's tiles are p + toff, tile j in slot j & 3 = ((j & 3) + toff) & 3; the PV at position 0
+    // is of the previous item's tile T-1+toff)
     constexpr int cv = (it == 0) ? ((T - 1) & 3) : ((c + 3) & 3);
-    const lds_char_t* pk = smem + kOffK + (c ^ toff) * kTile;
-    const lds_char_t* pv = smem + kOffV + (cv ^ toff) * kTile;
+    const lds_char_t* pk = smem + kOffK + ((c + toff) & 3) * kTile;
+    const lds_char_t* pv = smem + kOffV + ((cv + toff) & 3) * kTile;
     // every fragment is read in the phase that uses it, two k-steps ahead (nothing lives across
     // the VALU phase: the register budget holds the stream's staging); the first two K k-steps
     // are read at the phase start, their latency the only one exposed
@@ -613,6 +637,30 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    // this phase's LDS stores: the group's staging entries (stk_j / stv_j) and the next item's Q chunk.
+    // Issued after Sᵀ k-step 0 (hipcc keeps them in source order against the fragment reads: it cannot
+    // tell the slots apart), so the lgkmcnt(0) that publishes them at the phase end finds them done
+    auto lds_stores = [&]() __attribute__((always_inline)) {
+      static_for<0, stk_n(T, it)>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = decltype(I_)::value;
+        store(grp ? st_off(kOffK, stk_j(T, it, 1, i), stk_part(T, it, 1, i), kwo)
+                  : st_off(kOffK, stk_j(T, it, 0, i), stk_part(T, it, 0, i), kwo),
+              kst[i]);
+      });
+      static_for<0, stv_n(T, it)>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = decltype(I_)::value;
+        store(grp ? st_off(kOffV, stv_j(T, it, 1, i), stv_part(T, it, 1, i), vwo)
+                  : st_off(kOffV, stv_j(T, it, 0, i), stv_part(T, it, 0, i), vwo),
+              vst[i]);
+      });
+      if constexpr (it >= 3 && it <= 6) {
+        // the next item's Q chunk j = it-3 (channel rows 16j..16j+15) over the finished item's O,
+        // whose rows 16j.. both groups read out at MFMA(2 + j/2), an interval or more before
+        const int t = opaque_tid(), qc = t >> 5, qm2 = t & 31;
+        const uint32_t ql = qc * kQRow + ((qm2 * 16) ^ ((qc & 3) << 6));
+        store(((n + 1) & 1) * kQImg + ql + (it - 3) * 16 * kQRow, qst);
+      }
+    };
     half8 kf[4][2], vf[4][2];
     read_kstep(pk, 0, kf[0]);
     read_kstep(pk, 1, kf[1]);
@@ -623,6 +671,7 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[s][t], qf[s], s == 0 ? negm : st[t], 0, 0, 0);
       if (s < 2) read_kstep(pk, s + 2, kf[s + 2]);
       else read_vstep(pv, s - 2, vf[s - 2]);
+      if (s == 0) lds_stores();
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -635,10 +684,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       if (s < 2) read_vstep(pv, s + 2, vf[s + 2]);
     }
     __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // K k-steps 0-1
+    // this phase's LDS stores (staging, the next item's Q chunk) after Sᵀ k-step 0: done well before
+    // the lgkmcnt(0) that publishes them at the phase end
+    constexpr int nst = stk_n(T, it) + stv_n(T, it) + ((it >= 3 && it <= 6) ? 1 : 0);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {  // Sᵀ k-steps 0-1, each followed by a K k-step's reads
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      if (s == 0) __builtin_amdgcn_sched_group_barrier(0x200, nst, 0);
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {  // Sᵀ k-steps 2-3 and PV k-steps 0-1, each followed by a V k-step
@@ -646,25 +699,6 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // PV k-steps 2-3
-    // staging: K(+3), V(+2) into the ring; loads of K(+5), V(+4) (this item's or the next's)
-    // (the group's tiles of this position: stag_k1 / stag_v1, tile j in slot j & 3)
-    static_for<0, stag_nk(T, it)>([&](auto I_) __attribute__((always_inline)) {
-      constexpr int i = decltype(I_)::value, j0 = stag_k1(T, it, 0, i), j1 = stag_k1(T, it, 1, i);
-      const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
-      store(kOffK + (j & 3) * kTile + kwo, kst[i]);
-    });
-    static_for<0, stag_nv(T, it)>([&](auto I_) __attribute__((always_inline)) {
-      constexpr int i = decltype(I_)::value, j0 = stag_v1(T, it, 0, i), j1 = stag_v1(T, it, 1, i);
-      const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
-      store(kOffV + (j & 3) * kTile + vwo, vst[i]);
-    });
-    if constexpr (it >= 3 && it <= 6) {
-      // the next item's Q chunk j = it-3 (channel rows 16j..16j+15) over the finished item's O,
-      // whose rows 16j.. both groups read out at MFMA(2 + j/2), an interval or more before
-      const int t = opaque_tid(), qc = t >> 5, qm2 = t & 31;
-      const uint32_t ql = qc * kQRow + ((qm2 * 16) ^ ((qc & 3) << 6));
-      store(((n + 1) & 1) * kQImg + ql + (it - 3) * 16 * kQRow, qst);
-    }
     if constexpr (it == 2 || it == 3) {  // the finished item's O rows (at 2 also l / m); none before item 1
       const bool on = prv_q0 < nq;
       const lds_char_t* ob = smem + ((n + 1) & 1) * kQImg;
@@ -697,26 +731,19 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     }
     if constexpr (it >= 2 && it <= 5) qst = qload(nxt, it - 2);
     {
-      // the chunks the group stores at the next position (the next item's position 0 at T-1), one
-      // position ahead; tile j of the current item, or j - NT of the next
+      // the entries the group stores at the next position (the next item's position 0 at T-1), one
+      // position ahead (relative to the current item: + NT for the next item's)
       constexpr int pn = it + 1 < T ? it + 1 : 0, add = it + 1 < T ? 0 : NT;
-      auto src = [&](int j0, int j1, uint32_t slsz, int& slb, int& k0) __attribute__((always_inline)) {
-        const int j = (j0 == j1) ? j0 : (grp ? j1 : j0);
-        const bool nx = j >= NT;
-        slb = (nx ? nxt.sl : cur.sl) * (int)slsz;
-        k0 = (nx ? nxt.kt0 : cur.kt0) + (nx ? j - NT : j) * kBN;
-      };
-      static_for<0, stag_nk(T, pn)>([&](auto I_) __attribute__((always_inline)) {
+      auto rel = [](int j) constexpr { return j == kStDummy ? kStDummy : j + add; };
+      static_for<0, stk_n(T, pn)>([&](auto I_) __attribute__((always_inline)) {
         constexpr int i = decltype(I_)::value;
-        int slb, k0;
-        src(stag_k1(T, pn, 0, i) + add, stag_k1(T, pn, 1, i) + add, ksl, slb, k0);
-        kst[i] = load(krs, koff, (uint32_t)slb, k0);
+        kst[i] = st_load(krs, koff, koffp, ksl, rel(stk_j(T, pn, 0, i)), stk_part(T, pn, 0, i),
+                         rel(stk_j(T, pn, 1, i)), stk_part(T, pn, 1, i));
       });
-      static_for<0, stag_nv(T, pn)>([&](auto I_) __attribute__((always_inline)) {
+      static_for<0, stv_n(T, pn)>([&](auto I_) __attribute__((always_inline)) {
         constexpr int i = decltype(I_)::value;
-        int slb, k0;
-        src(stag_v1(T, pn, 0, i) + add, stag_v1(T, pn, 1, i) + add, vsl, slb, k0);
-        vst[i] = load(vrs, voff, (uint32_t)slb, k0);
+        vst[i] = st_load(vrs, voff, voffp, vsl, rel(stv_j(T, pn, 0, i)), stv_part(T, pn, 0, i),
+                         rel(stv_j(T, pn, 1, i)), stv_part(T, pn, 1, i));
       });
     }
     if constexpr (it == 0) {
@@ -726,6 +753,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         item_switch();
       }
     }
+    // publish this phase's staging stores before its barrier: the other group may read them in the
+    // next interval
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -796,8 +826,8 @@ thread_local TCache g_scache = {{}, 0, false};
 
 }  // namespace
 
-// positions T an item takes when group 1 runs two tiles ahead of group 0 (the first tile two before
-// group 1's first allowed key or at group 0's, whichever is lower); T + 2 a multiple of 4, >= kMinT
+// positions T an item takes when wave pair o runs o tiles ahead of pair 0 (the item's first tile o
+// below pair o's first, the lowest over the pairs); T + 3 a multiple of 4, >= kMinT
 int band_positions_stag(const FwdArgs& a) {
   if (g_scache.valid && !memcmp(&g_scache.r, &a.rule, sizeof(Rule))) return g_scache.T;
   const int nq = a.rule.q.n, nk = a.rule.k.n;
@@ -805,16 +835,17 @@ int band_positions_stag(const FwdArgs& a) {
   int T = 0;
   for (int qb = 0; qb < nqb; ++qb) {
     const int q0 = qb * kBM;
-    int kb0, ke0, kb1 = 0, ke1 = 0;
-    k_range_for_q_block(a.rule, q0, min(q0 + kBM / 2, nq) - 1, &kb0, &ke0);
-    const bool g1 = q0 + kBM / 2 < nq;
-    if (g1) k_range_for_q_block(a.rule, q0 + kBM / 2, min(q0 + kBM, nq) - 1, &kb1, &ke1);
-    int kt = ke0 > kb0 ? (kb0 / kBN) * kBN : nk;
-    if (g1 && ke1 > kb1) kt = min(kt, (kb1 / kBN) * kBN - 2 * kBN);
-    if (ke0 > kb0) T = max(T, (ke0 - kt + kBN - 1) / kBN);
-    if (g1 && ke1 > kb1) T = max(T, (ke1 - kt + kBN - 1) / kBN - 2);
+    int kb[4], ke[4], kt = nk;
+    for (int o = 0; o < 4; ++o) {
+      kb[o] = ke[o] = 0;
+      if (q0 + 64 * o >= nq) continue;
+      k_range_for_q_block(a.rule, q0 + 64 * o, min(q0 + 64 * o + 64, nq) - 1, &kb[o], &ke[o]);
+      if (ke[o] > kb[o]) kt = min(kt, (kb[o] / kBN) * kBN - o * kBN);
+    }
+    for (int o = 0; o < 4; ++o)
+      if (q0 + 64 * o < nq && ke[o] > kb[o]) T = max(T, (ke[o] - kt + kBN - 1) / kBN - o);
   }
-  T = (max(T, kMinT) + 2 + 3) / 4 * 4 - 2;
+  T = (max(T, kMinT) + 3 + 3) / 4 * 4 - 3;
   g_scache.r = a.rule;
   g_scache.T = T;
   g_scache.valid = true;
@@ -868,10 +899,10 @@ hipError_t launch_fwd_f16_band(const FwdArgs& a, hipStream_t s) {
   if (diag_variant("FA_FWD_VARIANT") == 2402) ba.inter = 0;
 #endif
   switch (ba.T) {
-    case 10: return launch_band_t<10>(ba, s);
-    case 14: return launch_band_t<14>(ba, s);
-    case 18: return launch_band_t<18>(ba, s);
-    default: return launch_band_t<22>(ba, s);
+    case 9: return launch_band_t<9>(ba, s);
+    case 13: return launch_band_t<13>(ba, s);
+    case 17: return launch_band_t<17>(ba, s);
+    default: return launch_band_t<21>(ba, s);
   }
 }
 
