@@ -339,6 +339,9 @@ def test_local_band_mfma(dtype, ws, causal, mode, nq, nk):
     ((2, 150), 776, 1552, 130, True, "scale_front", 48),
     ((300,), 1552, 520, 40, False, "scale_end", 64),
     ((2, 131), 1024, 1024, 700, True, "none_front", 64),
+    # the wider item instances (positions per item T = 17 and 21 of 9 / 13 / 17 / 21)
+    ((2, 9), 2048, 2048, 500, False, "none_front", 64),
+    ((3, 5), 2048, 2048, 600, False, "none_front", 64),
 ])
 def test_band_forward_persistent(batch, nq, nk, ws, causal, mode, d):
     b = int(np.prod(batch))
