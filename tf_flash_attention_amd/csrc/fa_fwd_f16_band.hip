@@ -280,8 +280,10 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
     const int t = opaque_tid(), qc = t >> 5, qq = 8 * (t & 31);
     const uint32_t qg = (uint32_t)qc * (uint32_t)nq * 2u + 2u * (uint32_t)qq;
     const bool in = qc + 16 * j < d && x.q0 + qq < nq;
+    // (nt: Q is read once; its lines should not push the band's K / V tiles, which the XCD's other
+    // workgroups re-read, out of the L2)
     return __builtin_amdgcn_raw_buffer_load_b128(qrs, in ? qg + (uint32_t)j * 32u * (uint32_t)nq : 0x80000000u,
-                                                 x.sl * qsl + 2 * min(x.q0, nq), 0);
+                                                 x.sl * qsl + 2 * min(x.q0, nq), 2);
   };
 
   // ---- staging entries (see stk_j / stv_j): the LDS place of entry (j, part) and its load
@@ -706,13 +708,14 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
       // the item's offsets are wave-uniform; readfirstlane proves it to hipcc (else every store below
       // is wrapped in a waterfall loop with an lgkmcnt(0) inside: cdna_hip_programming.md T20)
       const int osoff = __builtin_amdgcn_readfirstlane(prv_sl * osl + 2 * min(prv_q0, nq));
+      // (sc1: the written lines leave the L2 instead of displacing K / V tiles; O, l, m are not re-read)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int cc = orw + 16 * (2 * (it & 1) + j);
         const u32x4 v = *reinterpret_cast<const lds_u32x4_t*>(ob + cc * kQRow + 16 * ocl);
         const bool in = on && prv_q0 + 8 * ocl < nq;
         __builtin_amdgcn_raw_buffer_store_b128(v, ors, in ? (uint32_t)cc * (uint32_t)nq * 2u + 16u * ocl : 0x80000000u,
-                                               osoff, 0);
+                                               osoff, 16);
         store_data_guard();
       }
       if constexpr (it == 2) {
@@ -723,9 +726,9 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
         const uint32_t moff = (on && tt >= 64 && tt < 96 && prv_q0 + 8 * (tt - 64) < nq) ? 16u * (tt - 64) : 0x80000000u;
         const int lsoff = __builtin_amdgcn_readfirstlane(prv_sl * 4 * nq + 4 * min(prv_q0, nq));
         const int msoff = __builtin_amdgcn_readfirstlane(prv_sl * 2 * nq + 2 * min(prv_q0, nq));
-        __builtin_amdgcn_raw_buffer_store_b128(v, lrs, loff, lsoff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, lrs, loff, lsoff, 16);
         store_data_guard();
-        __builtin_amdgcn_raw_buffer_store_b128(v, mrs, moff, msoff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, mrs, moff, msoff, 16);
         store_data_guard();
       }
     }
