@@ -388,13 +388,14 @@ def test_wide_channels(dtype, d, vd, policy, ws, causal):
     run_case(dtype, policy, 1, "scale_front", (2,), d, vd, (97,), (150,), ws=ws, causal=causal, seed=d + vd)
 
 
-# fp16 forward for 128 < max(d, v_d) <= 256 on MFMA (fa_fwd_f16_wide.hip: full and interval rules,
-# nk % 8 == 0, aligned K / V): several key tiles, ragged query blocks, d != v_d, every sync mode
+# fp16 forward for 128 < max(d, v_d) <= 256 on MFMA (fa_fwd_f16_wide.hip, 16-B chunk staging: full and
+# interval rules, nk % 8 == 0, aligned K / V): several key tiles, ragged query blocks, d != v_d, every
+# sync mode
 @pytest.mark.parametrize("d,vd", [(256, 256), (160, 160), (130, 200), (200, 64), (64, 256)])
 @pytest.mark.parametrize("policy,mode,qs,ks,ws,causal", [
     ("full", "none_front", (300,), (520,), 1, False),
     # square causal, nk % 8 == 0 with a ragged query block: the wide MFMA kernel itself (heaviest
-    # blocks first, diagonal edge tiles on every block); 777 (nk % 8 != 0) runs the SIMT fallback
+    # blocks first, diagonal edge tiles on every block); 777 (nk % 8 != 0): its element-wise staging
     ("causal", "none_front", (776,), (776,), 1, False),
     ("causal", "none_front", (777,), (777,), 1, False),
     ("causal", "scale_end", (200,), (520,), 1, False),
@@ -460,6 +461,27 @@ def test_wide_channels_mfma_f64(d, vd, policy, seq, mode, qs, ks, ws, ls, causal
 ])
 def test_wide_channels_mfma_backward(d, vd, policy, seq, mode, qs, ks, ws, ls, causal):
     run_case(np.float16, policy, seq, mode, (2,), d, vd, qs, ks, ws=ws, ls=ls, causal=causal, seed=d + 5 * vd)
+
+
+# fp16 forward + backward for 128 < max(d, v_d) <= 256 on MFMA in the shapes the 16-B chunk staging
+# does not take (round 5; they ran on the SIMT kernels before): lengths not multiples of 8 and
+# misaligned tensors (element-wise staging: fa_fwd_f16_wide.hip ALN = false, the four-role backward
+# passes' ALN = false instances), and the rules that are not intervals (strided 1d and 2d local
+# windows: POL 2, per-element order checks on the edge tiles)
+@pytest.mark.parametrize("d,vd", [(256, 256), (160, 160), (200, 64)])
+@pytest.mark.parametrize("policy,seq,mode,qs,ks,ws,ls,causal,misalign", [
+    ("full", 1, "none_front", (131,), (197,), 1, 0, False, False),
+    ("causal", 1, "scale_end", (150,), (75,), 1, 0, False, False),
+    ("causal", 1, "none_front", (264,), (264,), 1, 0, False, True),
+    ("local", 1, "scale_front", (203,), (405,), 30, 0, True, False),
+    ("local", 1, "none_front", (150,), (150,), 20, 3, False, False),
+    ("local", 1, "none_front", (256,), (256,), 40, 2, True, False),
+    ("local", 2, "none_front", (9, 14), (9, 14), 4, 2, True, False),
+    ("local", 2, "none_front", (16, 24), (16, 24), 5, 0, False, False),
+])
+def test_wide_channels_mfma_general(d, vd, policy, seq, mode, qs, ks, ws, ls, causal, misalign):
+    run_case(np.float16, policy, seq, mode, (2,), d, vd, qs, ks, ws=ws, ls=ls, causal=causal,
+             seed=d + 17 * vd + ls, misalign=misalign)
 
 
 # --------------------------------------------------------------- edge cases

@@ -2258,9 +2258,13 @@ hipError_t launch_bwd_wide(const BwdArgs& a, hipStream_t s) {
   if constexpr (OC == 0) {  // the four-role pass: S / dP formed once per pair
     using S = W4Smem;
     const int64_t nkb = (a.rule.k.n + S::kBK - 1) / S::kBK;
-    const BwdKernel kern = pol == 0   ? bwd_dkdv_w4_kernel<0, true>
-                           : pol == 1 ? bwd_dkdv_w4_kernel<1, true>
-                                      : bwd_dkdv_w4_kernel<2, true>;
+    const bool aln = bwd_aligned(a);
+    const BwdKernel kern = aln ? (pol == 0   ? bwd_dkdv_w4_kernel<0, true>
+                                  : pol == 1 ? bwd_dkdv_w4_kernel<1, true>
+                                             : bwd_dkdv_w4_kernel<2, true>)
+                               : (pol == 0   ? bwd_dkdv_w4_kernel<0, false>
+                                  : pol == 1 ? bwd_dkdv_w4_kernel<1, false>
+                                             : bwd_dkdv_w4_kernel<2, false>);
     hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nkb)), dim3(512), S::kTotal, s, a);
@@ -2281,9 +2285,13 @@ hipError_t launch_bwd_wide(const BwdArgs& a, hipStream_t s) {
   if constexpr (OCQ == 0) {  // the four-role pass: Sᵀ / dPᵀ formed once per pair
     using S = W4DqSmem;
     const int64_t nqb = (a.rule.q.n + S::kBM - 1) / S::kBM;
-    const BwdKernel kern = pol == 0   ? bwd_dq_w4_kernel<0, true>
-                           : pol == 1 ? bwd_dq_w4_kernel<1, true>
-                                      : bwd_dq_w4_kernel<2, true>;
+    const bool aln = bwd_aligned(a);
+    const BwdKernel kern = aln ? (pol == 0   ? bwd_dq_w4_kernel<0, true>
+                                  : pol == 1 ? bwd_dq_w4_kernel<1, true>
+                                             : bwd_dq_w4_kernel<2, true>)
+                               : (pol == 0   ? bwd_dq_w4_kernel<0, false>
+                                  : pol == 1 ? bwd_dq_w4_kernel<1, false>
+                                             : bwd_dq_w4_kernel<2, false>);
     hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), S::kTotal);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(512), S::kTotal, s, a);
@@ -2325,7 +2333,7 @@ bool bwd_f16_fast_supported(const BwdArgs& a) {
   const int dm = max(a.d, a.v_d);
   // (buffer offsets are 32-bit: a channel row set of one slice stays below 2^31 bytes; the element-wise
   // staging of the unaligned form addresses up to 2·n + 14 bytes past a row start)
-  return dm >= 1 && (dm <= 128 || (dm <= 256 && bwd_aligned(a))) && nq > 0 && nk > 0 &&
+  return dm >= 1 && dm <= 256 && nq > 0 && nk > 0 &&
          (int64_t)dm * (nq + 8) * 2 < (1ll << 31) &&
          (int64_t)dm * (nk + 8) * 2 < (1ll << 31) && a.b * ((nk + 127) / 128) * 2 < (1ll << 31) &&
          a.b * ((nq + 127) / 128) * 2 < (1ll << 31);
@@ -2338,7 +2346,7 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
   if (e != hipSuccess) return e;
 #ifdef FA_DIAG
   // FA_BWD_VARIANT=1421: round 4's D = 256 dK/dV pass (two 128-channel chunks, S / dP formed in each)
-  if (max(a.d, a.v_d) > 128 && diag_variant("FA_BWD_VARIANT") == 1421) return launch_bwd_wide<2, 2>(a, s);
+  if (max(a.d, a.v_d) > 128 && bwd_aligned(a) && diag_variant("FA_BWD_VARIANT") == 1421) return launch_bwd_wide<2, 2>(a, s);
 #endif
   if (max(a.d, a.v_d) > 128) return launch_bwd_wide(a, s);
 #ifdef FA_DIAG

@@ -1,5 +1,8 @@
 // fa_fwd_f16_wide.hip — fp16 fused attention forward on MFMA for 128 < max(d, v_d) <= 256 (channels
-// zero-padded to 256), full policy and interval rules (causal, 1d unit-stride local windows).
+// zero-padded to 256), every rule: full (POL 0), interval rules (POL 1: causal, 1d unit-stride local
+// windows) and the other local windows (POL 2: strided, look-ahead, 2d; per-element order checks on
+// the edge tiles).  ALN: 16-B chunk staging (nk % 8 == 0, K / V 16-B aligned); otherwise the same
+// chunks are gathered element by element (zeros past nk), the LDS images unchanged.
 //
 // At 256 channels a 32-query x 64-key tile is 64 MFMAs (32 for Sᵀ = Kᵀ·Q over 16 channel k-steps,
 // 32 for Oᵀ += V·Pᵀ over 8 blocks of 32 output channels) against the same ~120 VALU instructions of
@@ -40,7 +43,7 @@ constexpr int kSmem = 4 * kTile;       // 128 KB (the Q image, 64 KB, aliases th
 constexpr int kCPT = kD * 8 / (kNW * 64);  // 16-B chunks of a tile per thread: 8
 constexpr float kRescaleThr = 8.f;
 
-template <int POL>
+template <int POL, bool ALN>
 __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_wide_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char_t* smem = (lds_char_t*)smem_raw;
@@ -76,19 +79,24 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_wide_kernel(FwdArgs a) {
 #pragma unroll
   for (int j = 0; j < kCPT; ++j) {
     const int c = (tid + kNW * 64 * j) >> 3;
-    const uint32_t go = (uint32_t)c * (uint32_t)nk * 2u + 16u * cm;
-    koff[j] = c < d ? go : 0x80000000u;
-    voff[j] = c < vd ? go : 0x80000000u;
+    const uint32_t go = (uint32_t)c * (uint32_t)nk * 2u + (ALN ? 16u * cm : 0u);
+    // (ALN: the row's chunk offset, 0x80000000 for a padding row; else the row start, checked per load)
+    koff[j] = (!ALN || c < d) ? go : 0x80000000u;
+    voff[j] = (!ALN || c < vd) ? go : 0x80000000u;
     kwo[j] = c * 128 + ((cm * 16) ^ ((c & 2) << 5));
     vwo[j] = kOffV + c * 128 + 16 * (cm ^ ((c >> 1) & 7));
   }
   // branch-free: chunks past nk (the tail, tiles past the end) read as zeros
-  auto load = [&](u32x4 (&dst)[kCPT], __amdgpu_buffer_rsrc_t rs, const uint32_t (&off)[kCPT], int k0)
+  auto load = [&](u32x4 (&dst)[kCPT], __amdgpu_buffer_rsrc_t rs, const uint32_t (&off)[kCPT], int rows, int k0)
       __attribute__((always_inline)) {
     const bool in = k0 + 8 * cm < nk;
 #pragma unroll
-    for (int j = 0; j < kCPT; ++j)
-      dst[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off[j] : 0x80000000u, 2 * min(k0, nk), 0);
+    for (int j = 0; j < kCPT; ++j) {
+      if constexpr (ALN)
+        dst[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, in ? off[j] : 0x80000000u, 2 * min(k0, nk), 0);
+      else
+        dst[j] = buf_load8h(rs, off[j], k0 + 8 * cm, nk, ((tid + kNW * 64 * j) >> 3) < rows);
+    }
   };
   auto store = [&](int base, const uint32_t (&wo)[kCPT], const u32x4 (&src)[kCPT]) __attribute__((always_inline)) {
 #pragma unroll
@@ -130,9 +138,9 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_wide_kernel(FwdArgs a) {
     __syncthreads();  // every wave has its fragments before the K ring overwrites the image
   }
   u32x4 stg[kCPT];
-  load(stg, krs, koff, kt0);
+  load(stg, krs, koff, d, kt0);
   store(0, kwo, stg);
-  load(stg, vrs, voff, kt0);
+  load(stg, vrs, voff, vd, kt0);
   store(0, vwo, stg);
   __syncthreads();
 
@@ -150,10 +158,16 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_wide_kernel(FwdArgs a) {
     wlo_max = __builtin_amdgcn_readlane(klo, last);
     whi_max = __builtin_amdgcn_readlane(khi, last);
   }
+  const int qo = (POL == 2) ? seq_order(a.rule.q, a.rule, min(qi, nq - 1)) : 0;  // this lane's query order
   // tile class for this wave: 0 no allowed pair (skipped), 1 mixed (masked), 2 all allowed
   auto tcls = [&](int it) -> int __attribute__((always_inline)) {
     const int k0 = kt0 + it * kBN, k1 = k0 + kBN - 1;
     if (POL == 0) return (k1 < nk) ? 2 : 1;
+    if (POL == 2) {  // (class 2 only for tiles wholly inside nk: the staged tail past nk is masked)
+      if (!wave_active || k0 >= nk) return 0;
+      const int c = tile_class(a.rule, wq0, min(wq0 + 31, nq - 1), k0, min(k1, nk - 1));
+      return (c == 2 && k1 >= nk) ? 1 : c;
+    }
     if (!wave_active || wlo_min > k1 || whi_max < k0) return 0;
     return (wlo_max <= k0 && whi_min >= k1 && k1 < nk) ? 2 : 1;
   };
@@ -186,7 +200,10 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_wide_kernel(FwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int off = 32 * t + 16 * (i >> 3) + (i & 7);
-        const bool ok = (POL == 1) ? ((unsigned)(base + off) < (unsigned)kspan) : (off < lim);
+        const int kk = k0 + 8 * h + off;
+        const bool ok = (POL == 1)   ? ((unsigned)(base + off) < (unsigned)kspan)
+                        : (POL == 2) ? (off < lim && check_orders_bf(a.rule, qo, seq_order(a.rule.k, a.rule, min(kk, nk - 1))))
+                                     : (off < lim);
         st[t][i] = ok ? st[t][i] : kNegInf;
       }
   };
@@ -284,10 +301,10 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_wide_kernel(FwdArgs a) {
   auto iter = [&](auto C_, int it) __attribute__((always_inline)) {
     constexpr int c = decltype(C_)::value;
     const int cls = (it < ntiles) ? tcls(it) : 0;
-    load(stg, krs, koff, kt0 + (it + 1) * kBN);
+    load(stg, krs, koff, d, kt0 + (it + 1) * kBN);
     if (cls != 0) qk(c);
     store((c ^ 1) * kTile, kwo, stg);
-    load(stg, vrs, voff, kt0 + (it + 1) * kBN);
+    load(stg, vrs, voff, vd, kt0 + (it + 1) * kBN);
     if (cls != 0) {
       softmax(it, cls);
       pv(c);
@@ -346,15 +363,18 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_wide_kernel(FwdArgs a) {
 bool fwd_f16_wide_supported(const FwdArgs& a) {
   const int nk = a.rule.k.n;
   const int dm = max(a.d, a.v_d);
-  return dm > 128 && dm <= kD && (nk % 8 == 0) && nk > 0 && (int64_t)dm * nk * 2 < (1ll << 31) &&
-         (int64_t)dm * a.rule.q.n * 2 < (1ll << 31) && (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) &&
-         (reinterpret_cast<uintptr_t>(a.V) % 16 == 0) && rule_is_interval(a.rule) &&
-         a.b * ((a.rule.q.n + kBM - 1) / kBM) < (1ll << 31);
+  // (32-bit buffer offsets: a slice's rows stay below 2^31 bytes, the element-wise gather included)
+  return dm > 128 && dm <= kD && nk > 0 && (int64_t)dm * (nk + 8) * 2 < (1ll << 31) &&
+         (int64_t)dm * a.rule.q.n * 2 < (1ll << 31) && a.b * ((a.rule.q.n + kBM - 1) / kBM) < (1ll << 31);
 }
 
 hipError_t launch_fwd_f16_wide(const FwdArgs& a, hipStream_t s) {
   const int64_t nqb = (a.rule.q.n + kBM - 1) / kBM;
-  auto kern = a.rule.policy == 0 ? fwd_f16_wide_kernel<0> : fwd_f16_wide_kernel<1>;
+  const bool aln = (a.rule.k.n % 8 == 0) && (reinterpret_cast<uintptr_t>(a.K) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(a.V) % 16 == 0);
+  const int pol = a.rule.policy == 0 ? 0 : rule_is_interval(a.rule) ? 1 : 2;
+  auto kern = aln ? (pol == 0 ? fwd_f16_wide_kernel<0, true> : pol == 1 ? fwd_f16_wide_kernel<1, true> : fwd_f16_wide_kernel<2, true>)
+                  : (pol == 0 ? fwd_f16_wide_kernel<0, false> : pol == 1 ? fwd_f16_wide_kernel<1, false> : fwd_f16_wide_kernel<2, false>);
   hipError_t e = set_smem_once(reinterpret_cast<const void*>(kern), kSmem);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.b * nqb)), dim3(kNW * 64), kSmem, s, a);

@@ -9,6 +9,9 @@ trace: no bwd_f16_kernel (single-pass, atomics) and no bwd_generic_kernel.
 
 With the argument f64 it runs fp64 forward + backward at 128 < D <= 256 over every rule class instead
 (the trace should show fwd_f64_kernel / bwd_dkdv_f64_kernel / bwd_dq_f64_kernel and no *_generic_*).
+With f16w: fp16 at 128 < D <= 256 in the shapes past the 16-B chunk staging and the interval rules
+(odd lengths, a misaligned pointer, strided 1d and 2d local windows): fwd_f16_wide_kernel and the
+four-role bwd_dkdv_w4_kernel / bwd_dq_w4_kernel only, no *_generic_*.
 """
 import os
 import sys
@@ -38,12 +41,23 @@ SHAPES_F64 = [
 ]
 
 
+SHAPES_F16W = [
+    ("full", 1, 256, (131,), (197,), 1, 0, False, False),
+    ("causal", 1, 160, (150,), (75,), 1, 0, False, False),
+    ("causal", 1, 256, (264,), (264,), 1, 0, False, True),
+    ("local", 1, 256, (150,), (150,), 20, 3, False, False),
+    ("local", 2, 200, (9, 14), (9, 14), 4, 2, True, False),
+    ("local", 2, 256, (16, 24), (16, 24), 5, 0, False, False),
+]
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    f64 = len(sys.argv) > 1 and sys.argv[1] == "f64"
-    dt = torch.float64 if f64 else torch.float16
-    for policy, sd, d, qs, ks, ws, ls, causal, mis in (SHAPES_F64 if f64 else SHAPES):
+    mode = sys.argv[1] if len(sys.argv) > 1 else ""
+    dt = torch.float64 if mode == "f64" else torch.float16
+    shapes = {"f64": SHAPES_F64, "f16w": SHAPES_F16W}.get(mode, SHAPES)
+    for policy, sd, d, qs, ks, ws, ls, causal, mis in shapes:
         def mk(shape):
             n = 1
             for x in shape:
