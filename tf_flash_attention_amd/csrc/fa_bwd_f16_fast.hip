@@ -946,15 +946,16 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_w4_kernel(BwdArgs a) {
     load_tile(qt0 + 32, 1);
     load_tile(qt0 + 64, 0);
   };
-  // the S / dP A operand of k-step s_ from a Q16 image (transposed reads)
-  auto read_op = [&](const lds_char_t* img, int s_) __attribute__((always_inline)) -> half8 {
+  // the S / dP A operand of k-step s_ from a Q16 image (transposed reads): a lane base per half e
+  // (q16_off(16 s + x) = 1024 s + q16_off(x) for x < 16), made opaque once per chain so hipcc adds the
+  // ring slot's offset in the step instead of keeping a base live for every (slot, half): as
+  // bwd_dq_w4_kernel, where those bases were spilled and reloaded every step
+  const uint32_t rb0 = q16_off(8 * (g >> 1) + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
+  const uint32_t rb1 = q16_off(8 * (g >> 1) + 4 + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
+  auto read_op = [&](const lds_char_t* img, const uint32_t (&rb)[2], int s_) __attribute__((always_inline)) -> half8 {
     half8 x;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const uint32_t off = q16_off(16 * s_ + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
-      const half4 t = tr_read(img + off);
-      if (e == 0) x.lo = t; else x.hi = t;
-    }
+    x.lo = tr_read(img + rb[0] + 1024 * s_);
+    x.hi = tr_read(img + rb[1] + 1024 * s_);
     return x;
   };
   // the resident B operand of a role A / B wave: X[c = 16s + 8h + j][key] from the K or V image
@@ -982,12 +983,14 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_w4_kernel(BwdArgs a) {
   // S / dP chain: 16 MFMAs, A operands two k-steps ahead
   auto chain = [&](const lds_char_t* img, const half8 (&xb)[D / 16], floatx16& acc) __attribute__((always_inline)) {
     constexpr int kS = D / 16, kAh = 2;
+    uint32_t rb[2] = {rb0, rb1};
+    asm volatile("" : "+v"(rb[0]), "+v"(rb[1]));
     half8 a8[kAh + 1];
 #pragma unroll
-    for (int s_ = 0; s_ < kAh; ++s_) a8[s_] = read_op(img, s_);
+    for (int s_ = 0; s_ < kAh; ++s_) a8[s_] = read_op(img, rb, s_);
 #pragma unroll
     for (int s_ = 0; s_ < kS; ++s_) {
-      if (s_ + kAh < kS) a8[(s_ + kAh) % (kAh + 1)] = read_op(img, s_ + kAh);
+      if (s_ + kAh < kS) a8[(s_ + kAh) % (kAh + 1)] = read_op(img, rb, s_ + kAh);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8[s_ % (kAh + 1)], xb[s_], acc, 0, 0, 0);
     }
   };
@@ -995,8 +998,11 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_w4_kernel(BwdArgs a) {
   auto accum = [&](const lds_char_t* img, const half8 (&z)[2], floatx16 (&acc)[D / 32]) __attribute__((always_inline)) {
     constexpr int kU = D / 32, kN = 2 * kU, kAh = 2;
     half8 y[kAh + 1];
+    // (row 32m + r: q16_off = 2048 m + q16_off(r); two opaque lane bases, one per unit, as read_op)
+    uint32_t gb[2] = {q16_off(r, h), q16_off(r, 2 + h)};
+    asm volatile("" : "+v"(gb[0]), "+v"(gb[1]));
     auto rd = [&](int n) __attribute__((always_inline)) {
-      y[n % (kAh + 1)] = read_b128(img + q16_off(32 * (n % kU) + r, 2 * (n / kU) + h));
+      y[n % (kAh + 1)] = read_b128(img + gb[n / kU] + 2048 * (n % kU));
     };
 #pragma unroll
     for (int n = 0; n < kAh; ++n) rd(n);
@@ -1322,14 +1328,16 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_w4_kernel(BwdArgs a) {
     load_tile(kt0 + 32, 1);
     load_tile(kt0 + 64, 0);
   };
-  auto read_op = [&](const lds_char_t* img, int s_) __attribute__((always_inline)) -> half8 {
+  // transposed A-operand reads of k-step s_: a lane base per half e (q16_off(16 s + x) = 1024 s +
+  // q16_off(x) for x < 16), made opaque once per chain so hipcc adds the slot's offset in the step
+  // instead of keeping a (slot, half) base live for every ring slot (it spilled them and reloaded them
+  // from scratch every step, with a vmcnt(0) that drained the staging loads)
+  const uint32_t rb0 = q16_off(8 * (g >> 1) + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
+  const uint32_t rb1 = q16_off(8 * (g >> 1) + 4 + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
+  auto read_op = [&](const lds_char_t* img, const uint32_t (&rb)[2], int s_) __attribute__((always_inline)) -> half8 {
     half8 x;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const uint32_t off = q16_off(16 * s_ + 8 * (g >> 1) + 4 * e + tq, 2 * (g & 1) + (sig >> 1), sig & 1);
-      const half4 t = tr_read(img + off);
-      if (e == 0) x.lo = t; else x.hi = t;
-    }
+    x.lo = tr_read(img + rb[0] + 1024 * s_);
+    x.hi = tr_read(img + rb[1] + 1024 * s_);
     return x;
   };
   auto resident = [&](int which, half8 (&xb)[D / 16]) __attribute__((always_inline)) {
@@ -1353,12 +1361,14 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_w4_kernel(BwdArgs a) {
   };
   auto chain = [&](const lds_char_t* img, const half8 (&xb)[D / 16], floatx16 acc) __attribute__((always_inline)) -> floatx16 {
     constexpr int kS = D / 16, kAh = 2;
+    uint32_t rb[2] = {rb0, rb1};
+    asm volatile("" : "+v"(rb[0]), "+v"(rb[1]));
     half8 a8[kAh + 1];
 #pragma unroll
-    for (int s_ = 0; s_ < kAh; ++s_) a8[s_] = read_op(img, s_);
+    for (int s_ = 0; s_ < kAh; ++s_) a8[s_] = read_op(img, rb, s_);
 #pragma unroll
     for (int s_ = 0; s_ < kS; ++s_) {
-      if (s_ + kAh < kS) a8[(s_ + kAh) % (kAh + 1)] = read_op(img, s_ + kAh);
+      if (s_ + kAh < kS) a8[(s_ + kAh) % (kAh + 1)] = read_op(img, rb, s_ + kAh);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8[s_ % (kAh + 1)], xb[s_], acc, 0, 0, 0);
     }
     return acc;
@@ -1465,8 +1475,11 @@ __global__ __launch_bounds__(512, 1) void bwd_dq_w4_kernel(BwdArgs a) {
       const lds_char_t* img = smem + ((c + 2) % 4) * S::kSlot + S::offKT;
       constexpr int kN = 2 * kU, kAh = 2;
       half8 y[kAh + 1];
+      // (row 32m + r: q16_off = 2048 m + q16_off(r); two opaque lane bases, one per unit, as read_op)
+      uint32_t gb[2] = {q16_off(r, h), q16_off(r, 2 + h)};
+      asm volatile("" : "+v"(gb[0]), "+v"(gb[1]));
       auto rd = [&](int n) __attribute__((always_inline)) {
-        y[n % (kAh + 1)] = read_b128(img + q16_off(32 * (kU * hh + n % kU) + r, 2 * (n / kU) + h));
+        y[n % (kAh + 1)] = read_b128(img + gb[n / kU] + 2048 * (kU * hh + n % kU));
       };
 #pragma unroll
       for (int n = 0; n < kAh; ++n) rd(n);
