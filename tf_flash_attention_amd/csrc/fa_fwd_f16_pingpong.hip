@@ -101,16 +101,6 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
   {
     // every load of the prologue in flight at once (the staging registers' too): one memory
     // latency before the loop instead of two
-    u32x4 kp[3], vp[2];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) kp[j] = load(krs, koff, j * kBN);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) vp[j] = load(vrs, voff, j * kBN);
-#pragma unroll
-    for (int j = 0; j < kNS; ++j) {
-      kst[j] = load(krs, koff, (3 + j) * kBN);
-      vst[j] = load(vrs, voff, (2 + j) * kBN);
-    }
     // Q [64][256], 64-B blocks XOR-swizzled by c&3: four chunks a thread, all loads before the stores
     // (a rolled loop here serialised four memory latencies: ~6000 cycles of prologue)
     constexpr int kQPT = kD * (kBM / 8) / (kNW * 64);
@@ -130,6 +120,18 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_pingpong_kernel(FwdArgs a
         const int idx = tid + j * kNW * 64, c = idx / (kBM / 8), m = idx % (kBM / 8);
         qv[j] = (c < d) ? load_chunk8(Q + (int64_t)c * nq, q0 + 8 * m, nq, false) : u32x4{0, 0, 0, 0};
       }
+    }
+    u32x4 kp[3], vp[2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) kp[j] = load(krs, koff, j * kBN);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) vp[j] = load(vrs, voff, j * kBN);
+    // the staging loads last: the stores below wait only for the loads before them (vmcnt drains in
+    // order), so the tiles three steps ahead stay in flight over the barrier
+#pragma unroll
+    for (int j = 0; j < kNS; ++j) {
+      kst[j] = load(krs, koff, (3 + j) * kBN);
+      vst[j] = load(vrs, voff, (2 + j) * kBN);
     }
 #pragma unroll
     for (int j = 0; j < kQPT; ++j) {
