@@ -484,6 +484,19 @@ def test_wide_channels_mfma_general(d, vd, policy, seq, mode, qs, ks, ws, ls, ca
              seed=d + 17 * vd + ls, misalign=misalign)
 
 
+# the same paths at their edges: fewer keys than one 16-B chunk, one query, fully masked rows (causal
+# scale_end with nq > nk), 129 channels, and a 2d window grid larger than a key tile
+@pytest.mark.parametrize("d,vd,policy,seq,mode,qs,ks,ws,ls,causal", [
+    (256, 256, "full", 1, "none_front", (37,), (5,), 1, 0, False),
+    (129, 129, "causal", 1, "none_front", (1,), (77,), 1, 0, False),
+    (200, 160, "causal", 1, "scale_end", (300,), (100,), 1, 0, False),
+    (256, 256, "local", 2, "scale_front", (21, 26), (42, 52), 6, 1, True),
+    (160, 256, "local", 1, "none_front", (519,), (519,), 64, 5, True),
+])
+def test_wide_channels_mfma_general_edges(d, vd, policy, seq, mode, qs, ks, ws, ls, causal):
+    run_case(np.float16, policy, seq, mode, (2,), d, vd, qs, ks, ws=ws, ls=ls, causal=causal, seed=d + vd + ws)
+
+
 # --------------------------------------------------------------- edge cases
 @pytest.mark.parametrize("dtype", DTYPES, ids=lambda t: np.dtype(t).name)
 @pytest.mark.parametrize("nq,nk", [(1, 1), (1, 77), (77, 1), (2, 3), (64, 64), (65, 63)])
