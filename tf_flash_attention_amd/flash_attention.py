@@ -350,3 +350,53 @@ def gradient_op_for(op_type: str):
     g = match.groupdict()
     name = f"{m.group(1).lower()}_attention_backward{g['ndim']}{'_float16' if g['f16'] else ''}"
     return getattr(_fa_kernel, name)
+
+
+# ----------------------------------------------------------------------------
+# The 'flops' statistic of each forward op (flash_attention.py:475-562 registers these with
+# ops.RegisterStatistics, so TF's profiler reports the op's algorithmic FLOPs)
+# ----------------------------------------------------------------------------
+_STAT_OPS = tuple(f"{p}AttentionForward{n}d{f}" for p in ("Full", "Causal", "Local") for n in (1, 2)
+                  for f in ("", "Float16"))
+
+
+def forward_flops_statistics(op_type: str, q_shape, k_shape, v_shape, attrs) -> float:
+    """The statistic the reference computes for a forward node (_estimate_{full,causal,local}_attention_
+    forward_flops, flash_attention.py:498-562): the op's Estimate*Flops over the node's Q/K/V shapes with
+    its sync_mode attr, and window_size / log2_stride_size / is_causal for the local ops.  Raises
+    ValueError('Unsupported op "..."') for any other op name, as the reference does."""
+    m = re.match(r"(Full|Causal|Local)AttentionForward(\d)d(Float16)?$", op_type)
+    if not m or m.group(2) not in ("1", "2"):
+        raise ValueError(f'Unsupported op "{op_type}"')
+    policy, seq_dims = m.group(1).lower(), int(m.group(2))
+    kw = {"sync_mode": attrs["sync_mode"]}
+    if policy == "local":
+        kw.update(window_size=int(attrs["window_size"]), log2_stride_size=int(attrs["log2_stride_size"]),
+                  is_causal=bool(attrs["is_causal"]))
+    return estimate_forward_flops(policy, seq_dims, tuple(q_shape), tuple(k_shape), tuple(v_shape), **kw)
+
+
+def register_tf_statistics() -> bool:
+    """With TensorFlow importable (the TF-ROCm op library of tf_op/ loaded), register
+    forward_flops_statistics as the 'flops' statistic of the 12 forward ops, as importing the
+    reference module does.  Returns False (nothing registered) when TensorFlow is absent."""
+    try:
+        from tensorflow.python.framework import ops as tf_ops  # noqa: WPS433 (optional dependency)
+    except ImportError:
+        return False
+
+    def _stat(graph, node):
+        def tensor(name):
+            return graph.get_tensor_by_name(name if ":" in name else name + ":0")
+        q, k, v = (tensor(node.input[i]) for i in range(3))
+        attrs = {"sync_mode": node.attr["sync_mode"].s.decode()}
+        if node.op.startswith("Local"):
+            attrs.update(window_size=node.attr["window_size"].i, log2_stride_size=node.attr["log2_stride_size"].i,
+                         is_causal=node.attr["is_causal"].b)
+        flops = forward_flops_statistics(node.op, q.shape.as_list(), k.shape.as_list(), v.shape.as_list(), attrs)
+        return tf_ops.OpStats("flops", flops)
+
+    for name in _STAT_OPS:
+        tf_ops.RegisterStatistics(name, "flops")(_stat)
+    return True
+
