@@ -2,7 +2,8 @@
 as test_gpu_parity.run_case): dtype, policy, 1d / 2d, sync mode, channel counts 1..256 (d != v_d),
 ragged and tiny lengths, window sizes and strides, look-ahead, misaligned tensors.  Each case is drawn
 from its own seed, so a failure names a reproducible case.  FA_FUZZ_N sets the number of cases (48 by
-default; the round-5 run of 400 is recorded in DESIGN.md §4)."""
+default; the round-5 runs are recorded in DESIGN.md §4); FA_FUZZ_LARGE=1 draws the reference tests'
+lengths (1d up to 4096, 2d up to 64 x 64) at d <= 128."""
 import os
 
 import numpy as np
@@ -13,6 +14,7 @@ from tests.test_gpu_parity import run_case
 pytestmark = pytest.mark.gpu
 
 N_CASES = int(os.environ.get("FA_FUZZ_N", "48"))
+LARGE = os.environ.get("FA_FUZZ_LARGE", "") == "1"  # lengths up to 4096 (1d) / 64 x 64 (2d), d <= 128
 CHANNELS = [1, 3, 8, 16, 24, 32, 48, 64, 65, 96, 100, 128, 129, 160, 200, 256]
 
 
@@ -22,16 +24,18 @@ def draw(i):
     policy = ["full", "causal", "local"][rng.integers(3)]
     seq = 1 if rng.random() < 0.7 else 2
     mode = ["none_front", "scale_front", "scale_end"][rng.integers(3)]
-    d = int(CHANNELS[rng.integers(len(CHANNELS))])
-    vd = d if rng.random() < 0.6 else int(CHANNELS[rng.integers(len(CHANNELS))])
+    chans = CHANNELS[:12] if LARGE else CHANNELS
+    d = int(chans[rng.integers(len(chans))])
+    vd = d if rng.random() < 0.6 else int(chans[rng.integers(len(chans))])
     if seq == 1:
-        lim = 700 if max(d, vd) <= 128 else 400
+        lim = 4097 if LARGE else (700 if max(d, vd) <= 128 else 400)
         qs = (int(rng.integers(1, lim)),)
         ks = (int(rng.integers(1, lim)),) if rng.random() < 0.6 else qs
     else:
-        qs = (int(rng.integers(1, 25)), int(rng.integers(1, 25)))
-        ks = (int(rng.integers(1, 25)), int(rng.integers(1, 25))) if rng.random() < 0.6 else qs
-    ws = int(rng.integers(1, 80 if seq == 1 else 10))
+        lim = 65 if LARGE else 25
+        qs = (int(rng.integers(1, lim)), int(rng.integers(1, lim)))
+        ks = (int(rng.integers(1, lim)), int(rng.integers(1, lim))) if rng.random() < 0.6 else qs
+    ws = int(rng.integers(1, (300 if LARGE else 80) if seq == 1 else 10))
     ls = int(rng.integers(0, 4)) if rng.random() < 0.5 else 0
     causal = bool(rng.random() < 0.5)
     misalign = bool(rng.random() < 0.15)
