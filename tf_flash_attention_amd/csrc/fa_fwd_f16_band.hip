@@ -616,11 +616,11 @@ __global__ __launch_bounds__(kNW * 64, 2) void fwd_f16_band_kernel(BandArgs ba) 
   const __amdgpu_buffer_rsrc_t lrs = make_rsrc(static_cast<float*>(a.l) + sl0 * (int64_t)nq, 4u * nq * nsl);
   const __amdgpu_buffer_rsrc_t mrs = make_rsrc(static_cast<__half*>(a.m) + sl0 * (int64_t)nq, 2u * nq * nsl);
 
-  // MFMA(it) (ring slot c = it mod 4): Sᵀ of the tile with K (k-steps 0-1 prefetched, 2-3 read
-  // here), PV of the previous tile with its V (read here, two k-steps ahead of their MFMAs), the
-  // next tile's K k-steps 0-1; staging: K(+3) / V(+2) into the ring over K(-1) / V(-2), loads of
-  // K(+5) / V(+4); the item's fixed-position traffic (O / l / m out at 2-3, the next item's Q in
-  // at 2-3 and into LDS at 4-5)
+  // MFMA(it): Sᵀ of the wave pair's tile it + toff (K k-steps 0-1 read at the phase head, 2-3 after
+  // the first MFMAs), PV of its previous tile (V read two k-steps ahead of its MFMAs); the group's
+  // staging entries of this position (stk_j / stv_j) stored after Sᵀ k-step 0 and the next
+  // position's loaded; the item's fixed-position traffic (O / l / m out at 2-3, the next item's Q
+  // loaded at 2-5 and stored into LDS at 3-6); an lgkmcnt(0) at the end publishes the stores
   auto mfma_phase = [&](auto IT_) __attribute__((always_inline)) {
     constexpr int it = decltype(IT_)::value;
     constexpr int c = it & 3;
