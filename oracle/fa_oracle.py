@@ -390,6 +390,59 @@ def backward_f64(Q, K, V, dO, prob: Problem, slices=None):
     return (dQ.reshape((n, d) + q_seq), dK.reshape((n, d) + k_seq), dV.reshape((n, vd) + k_seq))
 
 
+def backward_rounding_scale_f64(Q, K, V, dO, prob: Problem, u_t: float, u_acc: float, slices=None):
+    """Per-element rounding-error scale of the gradients (test infrastructure: the parity tests'
+    tolerance model, not a reference algorithm).  Each gradient is a sum of per-pair terms
+    (dQ = K·dSᵀ, dK = Q·dS, dV = dO·P, the same contractions as backward_f64); a term carries the
+    rounding of its factor dS (or P), and the returned scale is the root-sum-square over the sum
+    of |other factor| × that factor's error bound, the usual probabilistic bound for independent
+    roundings.  The error bound of one dS = P·(dP − D)·scale is
+        P·scale·( u_t·(1 + |s|_rss)·|dP − D| + u_t·|dO∘O|_rss + u_acc·Σ_c|dO_c·V_c| ),
+    with |s|_rss = scale·(Σ_c (q_c·k_c)²)^½ the scale of a score's rounding (Q is rounded to the tensor
+    type after scaling; the error scales P), |dO∘O|_rss the same for D (O is rounded to the tensor
+    type), u_t the tensor type's unit roundoff (dS and P are rounded to it) and u_acc that of the
+    accumulation: it grows where dP and D cancel, which a relative tolerance on the (small) result
+    cannot see.  P's error bound is u_t·(1 + |s|_rss)·P."""
+    bq, q_seq, k_seq, b, d, vd, nq, nk = _flat(Q, K, V, prob)
+    sl = list(range(b)) if slices is None else list(slices)
+    ev = _evaluator(prob, q_seq, k_seq)
+    q = Q.reshape(b, d, nq)
+    k = K.reshape(b, d, nk)
+    v = V.reshape(b, vd, nk)
+    do = dO.reshape(b, vd, nq)
+    scale = 1.0 / math.sqrt(d)
+    eQ = np.zeros((len(sl), d, nq)); eK = np.zeros((len(sl), d, nk)); eV = np.zeros((len(sl), vd, nk))
+    for r0, r1, c0, c1, mk in _row_chunks(ev, nq):
+        if c1 == c0:
+            continue
+        ha = mk.any(axis=1)
+        for j, i in enumerate(sl):
+            qi = q[i, :, r0:r1].astype(np.float64)
+            ki = k[i, :, c0:c1].astype(np.float64)
+            vi = v[i, :, c0:c1].astype(np.float64)
+            doi = do[i, :, r0:r1].astype(np.float64)
+            s = np.where(mk, (qi.T @ ki) * scale, -np.inf)
+            mrow = np.where(ha, s.max(axis=1), 0.0)
+            p = np.exp(s - mrow[:, None])
+            p = p / np.where(ha, p.sum(axis=1), 1.0)[:, None]
+            o = vi @ p.T
+            dp = doi.T @ vi
+            D = np.sum(doi * o, axis=0)
+            s_rss = np.sqrt((qi * qi).T @ (ki * ki)) * scale
+            e_p = u_t * (1.0 + s_rss) * p
+            e_ds = scale * (e_p * np.abs(dp - D[:, None])
+                            + p * (u_t * np.sqrt(np.sum((doi * o) ** 2, axis=0))[:, None]
+                                   + u_acc * (np.abs(doi).T @ np.abs(vi))))
+            eV[j, :, c0:c1] += (doi * doi) @ (e_p * e_p)
+            eQ[j, :, r0:r1] = (ki * ki) @ (e_ds * e_ds).T
+            eK[j, :, c0:c1] += (qi * qi) @ (e_ds * e_ds)
+    eQ, eK, eV = np.sqrt(eQ), np.sqrt(eK), np.sqrt(eV)
+    if slices is None:
+        return eQ.reshape(Q.shape), eK.reshape(K.shape), eV.reshape(V.shape)
+    n = len(sl)
+    return (eQ.reshape((n, d) + q_seq), eK.reshape((n, d) + k_seq), eV.reshape((n, vd) + k_seq))
+
+
 # ----------------------------------------------------------------------------
 # Algorithmic FLOP counts (SURVEY.md §8d) — allowed pairs from the rule
 # ----------------------------------------------------------------------------

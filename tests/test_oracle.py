@@ -196,6 +196,42 @@ def test_naive_backward_matches_f64_backward():
         np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
 
 
+def _bwd_f32_kernel_form(q, k, v, do):
+    """fp32 gradients in the kernels' formulation (Q pre-scaled, D = rowsum(dO*O) from the rounded O)."""
+    sc = np.float32(1.0 / math.sqrt(q.shape[0]))
+    s = (q * sc).astype(np.float32).T @ k
+    p = np.exp(s - s.max(axis=1, keepdims=True))
+    p /= p.sum(axis=1, keepdims=True)
+    D = np.sum(do * (v @ p.T), axis=0)
+    ds = p * (do.T @ v - D[:, None])
+    return (k @ ds.T) * sc, (q @ ds) * sc, do @ p
+
+
+@pytest.mark.parametrize("d,vd,nq,nk,seed", [(48, 48, 504, 1, 0), (8, 48, 200, 1, 5), (3, 200, 80, 2, 1),
+                                              (1, 128, 354, 2, 2), (16, 16, 70, 90, 3), (64, 64, 300, 300, 4)])
+def test_gradient_rounding_scale_covers_fp32(d, vd, nq, nk, seed):
+    """The gradient tolerance of the GPU parity tests (tests/test_gpu_parity.py: rtol/atol plus KAPPA x
+    backward_rounding_scale_f64) holds for a plain fp32 computation of the gradients in the kernels'
+    formulation, including the cancelling sums of a single key (dK analytically 0 from terms of size
+    ~|dP|), where that computation exceeds the rtol/atol part alone (checked: the model is needed)."""
+    from tests.test_gpu_parity import KAPPA, TOL, U_ROUND
+    rng = np.random.default_rng(seed)
+    q, k, v, do = (rng.uniform(-2, 2, s).astype(np.float32) for s in ((d, nq), (d, nk), (vd, nk), (vd, nq)))
+    prob = O.Problem("full", 1, "none_front")
+    got = _bwd_f32_kernel_form(q, k, v, do)
+    ref = O.backward_f64(q[None], k[None], v[None], do[None], prob)
+    esc = O.backward_rounding_scale_f64(q[None], k[None], v[None], do[None], prob, *U_ROUND[np.float32])
+    rtol, atol = TOL[np.float32]["bwd"]
+    base_ok = []
+    for g, r, e in zip(got, ref, esc):
+        r, e = r[0], e[0]
+        base = atol * max(np.abs(r).max(), 1.0) + rtol * np.abs(r)
+        assert (np.abs(g - r) <= base + KAPPA * e).all(), np.max(np.abs(g - r) / (base + KAPPA * e))
+        base_ok.append(bool((np.abs(g - r) <= base).all()))
+    if nk == 1:
+        assert not base_ok[1]   # dK of a single key: rtol/atol alone rejects a correct fp32 result
+
+
 def test_forward_rows_matches_forward():
     """forward_rows_f64 (row ranges of one long slice) equals forward_f64 on those rows."""
     rng = np.random.default_rng(12)
