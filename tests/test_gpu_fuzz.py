@@ -1,7 +1,7 @@
 """Seeded random sweep over the op's whole parameter space against the float64 oracle (the same check
 as test_gpu_parity.run_case): dtype, policy, 1d / 2d, sync mode, channel counts 1..256 (d != v_d),
 ragged and tiny lengths, window sizes and strides, look-ahead, misaligned tensors.  Each case is drawn
-from its own seed, so a failure names a reproducible case.  FA_FUZZ_N sets the number of cases (48 by
+from its own seed, so a failure names a reproducible case.  FA_FUZZ_N sets the number of cases (400 by
 default; the round-5 runs are recorded in DESIGN.md §4); FA_FUZZ_LARGE=1 draws the reference tests'
 lengths (1d up to 4096, 2d up to 64 x 64) at d <= 128."""
 import os
@@ -13,7 +13,7 @@ from tests.test_gpu_parity import run_case
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = int(os.environ.get("FA_FUZZ_N", "48"))
+N_CASES = int(os.environ.get("FA_FUZZ_N", "400"))
 LARGE = os.environ.get("FA_FUZZ_LARGE", "") == "1"  # lengths up to 4096 (1d) / 64 x 64 (2d), d <= 128
 CHANNELS = [1, 3, 8, 16, 24, 32, 48, 64, 65, 96, 100, 128, 129, 160, 200, 256]
 
