@@ -12,10 +12,11 @@ l is checked with the same rtol (l for fp16 is fp32), m to two units in the last
 place of T (it is the rounded row max) — for fp16 plus rtol 1e-3 / atol 1e-3*max(|m|,1),
 since the fp16 kernel scores with Q pre-scaled by scale*log2(e) in fp16; for fp32 / fp64 plus
 1e-6*|m| and the larger of 1e-6 (1e-12) and 2 eps of the score's rounding bound scale*|q|_1*max|k|.
-Gradients add KAPPA x the oracle's per-element rounding scale (see U_ROUND below), capped at the
-reference's own gate.  That gate
-(rtol=atol=1e-3*N for fp16, 1e-6*N otherwise; tests/test_base.py:198-226) is far
-looser and is implied.  Rows that attend nothing must be exactly O=0, l=0,
+Gradients add KAPPA x the oracle's per-element rounding scale (see U_ROUND below).
+The reference's own gate (rtol=atol=1e-3*N for fp16, 1e-6*N otherwise, N the K or Q entries;
+tests/test_base.py:198-226) is far looser at its tests' sizes; at N < 10 it is tighter than any
+of these and would reject a correct fp32 dQ of one or two keys (an analytic 0 formed from
+dP - D at ~1e-5), so it is not used as a cap.  Rows that attend nothing must be exactly O=0, l=0,
 m=bytes 0xFA.
 """
 
@@ -152,14 +153,9 @@ def run_case(dtype, policy, seq_dims, mode, batch, d, vd, qs, ks, ws=1, ls=0, ca
         dQ, dK, dV = O.backward_f64(Qf, Kf, Vf, dOf, prob, slices=sl)
         eQ, eK, eV = O.backward_rounding_scale_f64(Qf, Kf, Vf, dOf, prob, *U_ROUND[dtype], slices=sl)
         rtol, atol = TOL[dtype]["bwd"]
-        nk = int(np.prod(ks))
-        # capped at the reference's own gate for that gradient (tests/test_base.py:214-224: rtol = atol =
-        # c*N with N = the K entries for dQ, the Q entries for dK / dV, c = 1e-3 fp16, 1e-6 otherwise)
-        c = 1e-3 if dtype == np.float16 else 1e-6
-        ext = lambda e, r, n: np.minimum(KAPPA * e, c * n * (1.0 + np.abs(r)))  # noqa: E731
-        res["dQ"] = _close("dQ", flat(tq.grad.cpu().numpy())[sl], dQ, rtol, atol, ext(eQ, dQ, nk))
-        res["dK"] = _close("dK", flat(tk.grad.cpu().numpy())[sl], dK, rtol, atol, ext(eK, dK, nq))
-        res["dV"] = _close("dV", flat(tv.grad.cpu().numpy())[sl], dV, rtol, atol, ext(eV, dV, nq))
+        res["dQ"] = _close("dQ", flat(tq.grad.cpu().numpy())[sl], dQ, rtol, atol, KAPPA * eQ)
+        res["dK"] = _close("dK", flat(tk.grad.cpu().numpy())[sl], dK, rtol, atol, KAPPA * eK)
+        res["dV"] = _close("dV", flat(tv.grad.cpu().numpy())[sl], dV, rtol, atol, KAPPA * eV)
     return res
 
 
