@@ -57,3 +57,14 @@ def test_fuzz_case(i):
     c = draw(i)
     run_case(c["dtype"], c["policy"], c["seq_dims"], c["mode"], c["batch"], c["d"], c["vd"], c["qs"], c["ks"],
              ws=c["ws"], ls=c["ls"], causal=c["causal"], seed=c["seed"], misalign=c["misalign"])
+
+
+# seeds past the default range whose gradients are sums of large cancelling terms (one or two keys,
+# d = 1 scores): the cases that shaped the rounding scale of test_gpu_parity (profiles/r05_fuzz20000.txt,
+# r05_fuzz60000.txt), kept in the default suite
+CANCELLING = [4430, 5575, 5806, 11060, 12759, 14319, 16424, 17566, 19100, 19286, 19452, 32191, 50464, 53126]
+
+
+@pytest.mark.parametrize("i", CANCELLING, ids=_id)
+def test_fuzz_cancelling_case(i):
+    test_fuzz_case(i)
