@@ -38,9 +38,10 @@ TOL = {
 }
 # gradients also get KAPPA x the oracle's rounding-error scale (O.backward_rounding_scale_f64: the
 # root-sum-square of each term's rounding bound, for the tensor type's and the accumulation's unit
-# roundoff).  It matters only where a gradient is a sum of large cancelling terms — dK / dQ of a
+# roundoff).  It dominates where a gradient is a sum of large cancelling terms — dK / dQ of a
 # row set with one or two keys, dP ~ D — or where an fp16 score's rounding is large beside the
-# result (d = 1).  20000 seeded fuzz cases found fp32 errors of ~1.5e-5 against an exact 0 and fp16
+# result (d = 1).  Elsewhere it adds, at the worst element of a case, up to ~0.3x the rtol/atol
+# bound for fp32 and ~1-3x for fp16 (median element 0.1-0.5x: fp16 P and dS are rounded to 11 bits).  20000 seeded fuzz cases found fp32 errors of ~1.5e-5 against an exact 0 and fp16
 # ones of ~4e-2 at |dK| ~ 10 (d = 1, 354 queries on 2 keys); profiles/r05_fuzz20000.txt.
 U_ROUND = {np.float16: (2.0 ** -11, 2.0 ** -24), np.float32: (2.0 ** -24, 2.0 ** -24),
            np.float64: (2.0 ** -53, 2.0 ** -53)}
