@@ -290,9 +290,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
         qr[set][j] = buf_load8h(isO ? ors : qrs, voff[j], qa + 8 * cm_[j], nq, crow_[j] < (isO ? vd : d));
       }
     }
-    if (tid < 64) {  // lanes 0..31: lse2, 32..63: D
-      const int q = qa + (tid & 31);
-      lr[set] = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? -__builtin_huge_valf() : 0.f);
+    if (w == 0) {  // lanes 0..31: lse2, 32..63: D (wave-uniform branch; clamped load, select past nq)
+      const int q = qa + (lane & 31);
+      const float v = (lane < 32 ? glse : gD)[min(q, nq - 1)];
+      lr[set] = (q < nq) ? v : ((lane < 32) ? -__builtin_huge_valf() : 0.f);
     }
   };
   auto store_tile = [&](int slot, int set) {
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void bwd_dkdv_kernel(BwdArgs a) {
       lds_char_t* t = base + (isO ? S::offOT : S::offQT);
       *reinterpret_cast<lds_u32x4_t*>(t + q16_off(crow_[j], cm_[j])) = qr[set][j];
     }
-    if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr[set];
+    if (w == 0) reinterpret_cast<lds_f_t*>(base + S::offLse)[lane] = lr[set];
   };
 
   floatx16 dk[kDO / 32], dv[kDO / 32];
@@ -597,9 +598,11 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
         qr[set][j] = buf_load8h(isO ? ors : qrs, voff[j], qa + 8 * cm_[j], nq, crow_[j] < (isO ? vd : d));
       }
     }
-    if (tid < 64) {  // lanes 0..31: -lse2, 32..63: -D
-      const int q = qa + (tid & 31);
-      lr[set] = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? -__builtin_huge_valf() : 0.f);
+    if (w == 0) {  // lanes 0..31: -lse2, 32..63: -D (a wave-uniform scalar branch; the load itself is
+                   // unconditional, clamped into the row, and the select replaces rows past nq)
+      const int q = qa + (lane & 31);
+      const float v = (lane < 32 ? glse : gD)[min(q, nq - 1)];
+      lr[set] = (q < nq) ? v : ((lane < 32) ? -__builtin_huge_valf() : 0.f);
     }
   };
   auto store_tile = [&](int slot, int set) __attribute__((always_inline)) {
@@ -609,7 +612,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_pc_kernel(BwdArgs a) {
       const bool isO = is_o(j);
       *reinterpret_cast<lds_u32x4_t*>(base + (isO ? S::offOT : S::offQT) + q16_off(crow_[j], cm_[j])) = qr[set][j];
     }
-    if (tid < 64) reinterpret_cast<lds_f_t*>(base + (tid < 32 ? S::offLse : S::offD - 128))[tid] = lr[set];
+    if (w == 0) reinterpret_cast<lds_f_t*>(base + (lane < 32 ? S::offLse : S::offD - 128))[lane] = lr[set];
   };
   // hand-over slot of this wave pair: four b128 per lane (P k-steps 0/1, dS k-steps 0/1), lane-linear
   auto xoff = [&](int xs, int j) -> uint32_t { return S::offX + xs * S::kXSlot + wl * S::kXWave + j * 1024 + lane * 16; };
@@ -956,9 +959,10 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_w4_kernel(BwdArgs a) {
         qr[set][j] = buf_load8h(isO ? ors : qrs, voff[j], qa + 8 * cm_[j], nq, crow_[j] < (isO ? vd : d));
       }
     }
-    if (tid < 64) {  // lanes 0..31: -lse2, 32..63: -D
-      const int q = qa + (tid & 31);
-      lr[set] = (q < nq) ? ((tid < 32) ? glse[q] : gD[q]) : ((tid < 32) ? -__builtin_huge_valf() : 0.f);
+    if (w == 0) {  // lanes 0..31: -lse2, 32..63: -D (wave-uniform branch; clamped load, select past nq)
+      const int q = qa + (lane & 31);
+      const float v = (lane < 32 ? glse : gD)[min(q, nq - 1)];
+      lr[set] = (q < nq) ? v : ((lane < 32) ? -__builtin_huge_valf() : 0.f);
     }
   };
   auto store_tile = [&](int slot, int set) __attribute__((always_inline)) {
@@ -968,7 +972,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_w4_kernel(BwdArgs a) {
       const bool isO = is_o(j);
       *reinterpret_cast<lds_u32x4_t*>(base + (isO ? S::offOT : S::offQT) + q16_off(crow_[j], cm_[j])) = qr[set][j];
     }
-    if (tid < 64) reinterpret_cast<lds_f_t*>(base + S::offLse)[tid] = lr[set];
+    if (w == 0) reinterpret_cast<lds_f_t*>(base + S::offLse)[lane] = lr[set];
   };
   // hand-over of this slice: two b128 per lane (k-steps 0 / 1), lane-linear
   auto poff = [&](int xs, int j) -> uint32_t { return S::offP + (2 * xs + sl) * S::kXW + j * 1024 + lane * 16; };
