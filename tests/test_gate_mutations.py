@@ -1,0 +1,163 @@
+"""The gradient gate of the GPU parity tests rejects real defects.
+
+`tests/test_gpu_parity.run_case` accepts a gradient element when
+    |got - ref| <= atol*max(max|ref|, 1) + rtol*|ref| + KAPPA * e          (gate.grad_bound)
+with e the oracle's rounding-error scale (oracle.backward_rounding_scale_f64).  The rounding term is
+what lets a correct fp16 / fp32 computation through where a gradient is a sum of large cancelling
+terms; this file checks, on the CPU, that the same gate still rejects gradients computed with an
+injected defect of the kinds a flash-attention backward can have:
+
+  drop_key_tile_dq     dQ misses one 64-key tile's contribution (a skipped tile in the dQ pass)
+  drop_q_tile_dkdv     dK and dV miss one 64-query tile's contribution (a skipped tile in dK/dV)
+  ds_scale             dS scaled by 1 + 2^-8
+  d_neighbour          D = rowsum(dO*O) taken from the neighbouring query row
+  attend_masked        one pair the rule masks is attended (P renormalised over it)
+  lse_ulp              P normalised with m off by one fp16 ulp (P scaled by exp(ulp(m)) per row)
+
+Defective gradients are formed exactly (float64) from the same dtype-rounded inputs as the reference,
+then rounded to the tensor type as a kernel's output is, and passed through the gate code the GPU
+tests use.  Shapes: the 14 seeds whose cancelling sums shaped the rounding model
+(test_gpu_fuzz.CANCELLING) and sweep shapes from the default fuzz draw, each in fp16 and fp32.
+The reference test suite's own gate is /root/reference/flash_attention/tests/test_base.py:198-226."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import fa_oracle as O
+from tests import gate
+from tests.test_gpu_fuzz import CANCELLING, draw
+
+MUTATIONS = ["drop_key_tile_dq", "drop_q_tile_dkdv", "ds_scale", "d_neighbour", "attend_masked", "lse_ulp"]
+# sweep cases of the default draw with at least 2 query and key tiles' worth of work, mixed policies
+SWEEP = [i for i in range(400) if draw(i)["seq_dims"] == 1 and min(draw(i)["qs"][0], draw(i)["ks"][0]) >= 130][:10]
+
+
+def _inputs(c, dtype):
+    rng = np.random.default_rng(c["seed"])
+    qs, ks, batch = tuple(c["qs"]), tuple(c["ks"]), tuple(c["batch"])
+    Q = rng.uniform(-2, 2, batch + (c["d"],) + qs).astype(dtype)
+    K = rng.uniform(-2, 2, batch + (c["d"],) + ks).astype(dtype)
+    V = rng.uniform(-2, 2, batch + (c["vd"],) + ks).astype(dtype)
+    dO = rng.uniform(-2, 2, batch + (c["vd"],) + qs).astype(dtype)
+    return Q, K, V, dO
+
+
+def _mutated_grads(q, k, v, do, mask, mut, dtype):
+    """Gradients of one slice (float64) with defect `mut`; None when the shape cannot hold it."""
+    d, nq = q.shape
+    nk = k.shape[1]
+    scale = 1.0 / math.sqrt(d)
+    mask = mask.copy()
+    if mut == "attend_masked":
+        rows = np.nonzero(mask.any(axis=1) & ~mask.all(axis=1))[0]
+        if rows.size == 0:
+            return None
+        i = rows[rows.size // 2]
+        j = np.nonzero(~mask[i])[0]
+        j = j[np.argmin(np.abs(j - np.nonzero(mask[i])[0].mean()))]  # the masked key nearest the row's keys
+        mask[i, j] = True
+    if mut == "d_neighbour" and nq < 2:
+        return None
+    ha = mask.any(axis=1)
+    s = np.where(mask, (q.T @ k) * scale, -np.inf)
+    mrow = np.where(ha, s.max(axis=1), 0.0)
+    p = np.exp(s - mrow[:, None])
+    p = p / np.where(ha, p.sum(axis=1), 1.0)[:, None]
+    if mut == "lse_ulp":
+        # the stored m is fp16; one ulp of it (natural-log units) wrong in the normaliser
+        ulp = np.abs(np.spacing(np.abs(mrow).astype(np.float16))).astype(np.float64)
+        p = p * np.exp(ulp)[:, None]
+    o = v @ p.T
+    D = np.sum(do * o, axis=0)
+    if mut == "d_neighbour":
+        D = np.concatenate([D[1:], D[-2:-1]])
+    dp = do.T @ v
+    ds = p * (dp - D[None, :].T) * scale
+    if mut == "ds_scale":
+        ds = ds * (1.0 + 2.0 ** -8)
+    dq, dk, dv = k @ ds.T, q @ ds, do @ p
+    if mut == "drop_key_tile_dq":
+        t = (nk // 64) // 2
+        sl = slice(64 * t, min(nk, 64 * t + 64))
+        dq = dq - k[:, sl] @ ds[:, sl].T
+    if mut == "drop_q_tile_dkdv":
+        t = (nq // 64) // 2
+        sl = slice(64 * t, min(nq, 64 * t + 64))
+        dk = dk - q[:, sl] @ ds[sl, :]
+        dv = dv - do[:, sl] @ p[sl, :]
+    return [g.astype(dtype).astype(np.float64) for g in (dq, dk, dv)]
+
+
+def _case(c, dtype):
+    Q, K, V, dO = _inputs(c, dtype)
+    prob = O.Problem(c["policy"], c["seq_dims"], c["mode"], c["ws"], c["ls"], c["causal"])
+    b = int(np.prod(c["batch"]))
+    flat = lambda x: x.reshape((b,) + x.shape[len(c["batch"]):])  # noqa: E731
+    Qf, Kf, Vf, dOf = flat(Q), flat(K), flat(V), flat(dO)
+    ref = O.backward_f64(Qf, Kf, Vf, dOf, prob)
+    esc = O.backward_rounding_scale_f64(Qf, Kf, Vf, dOf, prob, *gate.U_ROUND[dtype])
+    mask = O.problem_mask(prob, tuple(c["qs"]), tuple(c["ks"]))
+    d, vd, nq, nk = c["d"], c["vd"], int(np.prod(c["qs"])), int(np.prod(c["ks"]))
+    return Qf, Kf, Vf, dOf, ref, esc, mask, (d, vd, nq, nk)
+
+
+def _rejected(case, mut, dtype):
+    """True / False: the gate rejects / accepts the defect; None: not applicable to the case."""
+    Qf, Kf, Vf, dOf, ref, esc, mask, (d, vd, nq, nk) = case
+    got = [[], [], []]
+    for i in range(Qf.shape[0]):
+        g = _mutated_grads(Qf[i].reshape(d, nq).astype(np.float64), Kf[i].reshape(d, nk).astype(np.float64),
+                           Vf[i].reshape(vd, nk).astype(np.float64), dOf[i].reshape(vd, nq).astype(np.float64),
+                           mask, mut, dtype)
+        if g is None:
+            return None
+        for j in range(3):
+            got[j].append(g[j])
+    ok, material = True, False
+    rtol, atol = gate.TOL[dtype]["bwd"]
+    for j, name in enumerate(("dQ", "dK", "dV")):
+        r = ref[j].reshape(len(got[j]), -1)
+        e = esc[j].reshape(len(got[j]), -1)
+        g = np.stack(got[j]).reshape(r.shape)
+        ok &= gate.grad_ok(g, r, e, dtype)
+        # material: visible to an exact computation at all — past the plain rtol/atol bound somewhere,
+        # or past the slope tolerance (a defect below both is below fp rounding of the case, e.g. a dropped
+        # tile of keys no query attends to, or dS scaled where dS is analytically 0)
+        material |= bool((np.abs(g - r) > gate.plain_bound(r, rtol, atol)).any())
+        material |= gate.slope_applies(r, e) and abs(gate.scale_slope(g, r)) > gate.SLOPE_TOL[dtype]
+    if not material:
+        return None
+    return not ok
+
+
+def _cases():
+    out = []
+    for i in CANCELLING + SWEEP:
+        for dt in (np.float16, np.float32):
+            out.append((i, dt))
+    return out
+
+
+@pytest.mark.parametrize("i,dtype", _cases(), ids=lambda x: str(x) if isinstance(x, int) else np.dtype(x).name)
+def test_gate_rejects_defects(i, dtype):
+    c = draw(i)
+    case = _case(c, dtype)
+    passed = []
+    for mut in MUTATIONS:
+        r = _rejected(case, mut, dtype)
+        if r is False:
+            passed.append(mut)
+    assert not passed, f"case {i} ({np.dtype(dtype).name}): the gradient gate accepts {passed}"
+
+
+def test_correct_gradients_pass_gate():
+    """The same gate accepts the exact gradients rounded to the tensor type (sanity of the harness)."""
+    for i in CANCELLING[:4]:
+        c = draw(i)
+        for dt in (np.float16, np.float32):
+            Qf, Kf, Vf, dOf, ref, esc, mask, _ = _case(c, dt)
+            for j in range(3):
+                g = ref[j].astype(dt).astype(np.float64)
+                assert gate.grad_ok(g.reshape(g.shape[0], -1), ref[j].reshape(g.shape[0], -1),
+                                    esc[j].reshape(g.shape[0], -1), dt)

@@ -14,6 +14,7 @@ from tests.test_gpu_parity import run_case
 pytestmark = pytest.mark.gpu
 
 N_CASES = int(os.environ.get("FA_FUZZ_N", "400"))
+START = int(os.environ.get("FA_FUZZ_START", "0"))  # (long sweeps run in slices: cases START .. N_CASES-1)
 LARGE = os.environ.get("FA_FUZZ_LARGE", "") == "1"  # lengths up to 4096 (1d) / 64 x 64 (2d), d <= 128
 CHANNELS = [1, 3, 8, 16, 24, 32, 48, 64, 65, 96, 100, 128, 129, 160, 200, 256]
 
@@ -52,7 +53,7 @@ def _id(i):
             + ("-mis" if c["misalign"] else ""))
 
 
-@pytest.mark.parametrize("i", range(N_CASES), ids=_id)
+@pytest.mark.parametrize("i", range(START, N_CASES), ids=_id)
 def test_fuzz_case(i):
     c = draw(i)
     run_case(c["dtype"], c["policy"], c["seq_dims"], c["mode"], c["batch"], c["d"], c["vd"], c["qs"], c["ks"],

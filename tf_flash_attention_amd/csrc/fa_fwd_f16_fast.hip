@@ -492,6 +492,7 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
   const int v = diag_variant("FA_FWD_VARIANT");
   if (fwd_f16_pp_supported(a) && v >= 2000 && v < 2200) return launch_fwd_f16_pp(a, s);  // 21xx: its ablations
   if (fwd_f16_pingpong_supported(a) && v == 2200) return launch_fwd_f16_pingpong(a, s);
+  if (fwd_f16_gap_supported(a) && v >= 2600 && v < 2700) return launch_fwd_f16_gap(a, s);  // 26xx: its ablations
   if (fwd_f16_pingpong128_supported(a) && v == 2301) return launch_fwd_f16_pingpong128(a, s);
   if (d64 && v == 1814) return launch_fast_t<64, 8, kFPrio | kFLateV | kFTpb2>(a, s);
   if (v == 146) return d64 ? launch_fast_t<64, 4, kFPrio | kFLateV>(a, s) : launch_fast_t<128, 4, kFPrio | kFLateV>(a, s);

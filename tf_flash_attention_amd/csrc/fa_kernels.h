@@ -61,6 +61,10 @@ hipError_t launch_fwd_f16_pp(const FwdArgs& a, hipStream_t s);
 // ping-pong fp16 forward (8 waves, two groups alternating MFMA / softmax phases) — fa_fwd_f16_pingpong.hip
 bool fwd_f16_pingpong_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s);
+// one-wave-per-SIMD fp16 forward with a hand-placed gap stream, full policy, 32 < max(d, v_d) <= 64 —
+// diag/fa_fwd_f16_gap.hip (diagnostic library only: FA_FWD_VARIANT 26xx)
+bool fwd_f16_gap_supported(const FwdArgs& a);
+hipError_t launch_fwd_f16_gap(const FwdArgs& a, hipStream_t s);
 // ping-pong fp16 forward for 64 < max(d, v_d) <= 128 — fa_fwd_f16_pingpong128.hip
 bool fwd_f16_pingpong128_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_pingpong128(const FwdArgs& a, hipStream_t s);
