@@ -355,6 +355,13 @@ def test_local_band_mfma(dtype, ws, causal, mode, nq, nk):
     # the wider item instances (positions per item T = 17 and 21 of 9 / 13 / 17 / 21)
     ((2, 9), 2048, 2048, 500, False, "none_front", 64),
     ((3, 5), 2048, 2048, 600, False, "none_front", 64),
+    # small windows with nq not a multiple of the 256-query block: the first item's wave-pair
+    # ranges start at key tiles below 0 (zero-filled loads, dummy stagger entries, class-0 tiles)
+    ((3, 7), 1000, 1000, 40, False, "none_front", 64),
+    ((3, 7), 1000, 1000, 40, True, "none_front", 64),
+    ((4, 5), 264, 264, 8, False, "none_front", 64),
+    ((4, 5), 264, 264, 8, True, "none_front", 64),
+    ((2, 3), 1000, 1000, 40, True, "scale_front", 64),
 ])
 def test_band_forward_persistent(batch, nq, nk, ws, causal, mode, d):
     b = int(np.prod(batch))

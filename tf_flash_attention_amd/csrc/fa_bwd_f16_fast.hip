@@ -2313,8 +2313,8 @@ hipError_t launch_dq(const BwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// 128 < max(d, v_d) <= 256 (16-B aligned tensors, lengths multiples of 8): both one-wave passes at D =
-// 256, each workgroup on one of two 128-channel output chunks
+// 128 < max(d, v_d) <= 256, any alignment and length (the ALN = false instances stage element-wise):
+// the passes at D = 256
 // OC / OCQ = 0: the four-role dK / dV / dQ passes; > 0: the one-wave passes on that many output-channel
 // chunks (round 4's structure, FA_BWD_VARIANT=1421)
 template <int OC = 0, int OCQ = 0>

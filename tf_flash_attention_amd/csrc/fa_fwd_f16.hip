@@ -488,7 +488,7 @@ bool fwd_f16_supported(const FwdArgs& a) {
 
 hipError_t launch_fwd_f16(const FwdArgs& a, hipStream_t s) {
   const int dm = max(a.d, a.v_d);
-  // 128 < max(d, v_d) <= 256 under the full / interval rules with aligned K, V: 256-channel MFMA tiles
+  // 128 < max(d, v_d) <= 256, every rule and alignment: 256-channel MFMA tiles (fa_fwd_f16_wide.hip)
   if (dm > 128) return launch_fwd_f16_wide(a, s);
 #ifdef FA_DIAG
   // FA_FWD_VARIANT = <NW><F> below 1000 pins this general kernel (A/B runs), e.g. 408

@@ -68,7 +68,9 @@ hipError_t launch_fwd_f16_gap(const FwdArgs& a, hipStream_t s);
 // ping-pong fp16 forward for 64 < max(d, v_d) <= 128 — fa_fwd_f16_pingpong128.hip
 bool fwd_f16_pingpong128_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_pingpong128(const FwdArgs& a, hipStream_t s);
-// fp16 forward on MFMA for 128 < max(d, v_d) <= 256, full / interval rules — fa_fwd_f16_wide.hip
+// fp16 forward on MFMA for 128 < max(d, v_d) <= 256: every rule (interval rules by key ranges, strided /
+// 2d windows by per-element masks) and any alignment or length (element-wise staging where K / V are not
+// 16-B aligned) — fa_fwd_f16_wide.hip
 bool fwd_f16_wide_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_wide(const FwdArgs& a, hipStream_t s);
 // persistent band forward for 1d unit-stride local windows, 32 < max(d, v_d) <= 64 — fa_fwd_f16_band.hip
