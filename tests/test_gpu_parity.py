@@ -12,7 +12,8 @@ l is checked with the same rtol (l for fp16 is fp32), m to two units in the last
 place of T (it is the rounded row max) — for fp16 plus rtol 1e-3 / atol 1e-3*max(|m|,1),
 since the fp16 kernel scores with Q pre-scaled by scale*log2(e) in fp16; for fp32 / fp64 plus
 1e-6*|m| and the larger of 1e-6 (1e-12) and 2 eps of the score's rounding bound scale*|q|_1*max|k|.
-Gradients add KAPPA x the oracle's per-element rounding scale (tests/gate.py).
+Gradients add KAPPA x the oracle's per-element rounding scale (capped in fp16 where the element does
+not cancel) and must pass the whole-gradient scale-slope check (tests/gate.py).
 The reference's own gate (rtol=atol=1e-3*N for fp16, 1e-6*N otherwise, N the K or Q entries;
 tests/test_base.py:198-226) is far looser at its tests' sizes; at N < 10 it is tighter than any
 of these and would reject a correct fp32 dQ of one or two keys (an analytic 0 formed from
@@ -157,6 +158,10 @@ def run_case(dtype, policy, seq_dims, mode, batch, d, vd, qs, ks, ws=1, ls=0, ca
                     f.write(json.dumps(st) + "\n")
         for name, (got, ref, e) in grads.items():
             res[name] = _close(name, got, ref, rtol, atol, gate.grad_extra(ref, e, dtype))
+            # whole-gradient scale: catches a defect scaling a gradient by ~2^-8 in fp16 that the
+            # per-element bound cannot see (tests/gate.py, tests/test_gate_mutations.py)
+            assert gate.slope_ok(got, ref, e, dtype), (
+                f"{name}: scale slope {gate.scale_slope(got, ref):.3e} > {gate.SLOPE_TOL[dtype]:.3e}")
     return res
 
 
@@ -662,6 +667,28 @@ def test_f16_forward_structures_d128(monkeypatch, diag_lib, variant, policy, seq
     monkeypatch.setenv("FA_FWD_VARIANT", variant)
     run_case(np.float16, policy, seq_dims, mode, (2, 2), d + 64, vd + 32, qs, ks, ws=ws, ls=0, causal=causal,
              bwd=False, seed=int(variant) + d + ws)
+
+
+# the 64-keys-a-wave dK/dV pass (csrc/diag/fa_bwd_f16_k64.hip, FA_BWD_VARIANT=1700): full, causal and
+# 1d local windows at d in (64, 128], lengths off the 256-key block and the 32-query tile, nq != nk
+K64_CASES = [
+    ("full", "none_front", (264,), (520,), 1, False, 128, 128),
+    ("causal", "none_front", (600,), (600,), 1, False, 128, 128),
+    ("causal", "scale_end", (328,), (776,), 1, False, 96, 128),
+    ("local", "none_front", (1000,), (1000,), 70, False, 128, 128),
+    ("local", "scale_front", (520,), (264,), 40, True, 128, 80),
+    ("full", "none_front", (64,), (8,), 1, False, 128, 128),
+]
+
+
+@pytest.mark.parametrize("policy,mode,qs,ks,ws,causal,d,vd", K64_CASES)
+def test_f16_backward_k64(monkeypatch, diag_lib, policy, mode, qs, ks, ws, causal, d, vd):
+    monkeypatch.setenv("FA_BWD_VARIANT", "1700")
+    calls = diag_lib.fa_diag_call_count
+    calls.restype = __import__("ctypes").c_longlong
+    before = calls(1)
+    run_case(np.float16, policy, 1, mode, (2, 2), d, vd, qs, ks, ws=ws, ls=0, causal=causal, seed=1700 + d + ws)
+    assert calls(1) == before + 1
 
 
 # backward structures kept in the diagnostic library: 1599 = the one-wave dQ pass (the structure the

@@ -2439,6 +2439,11 @@ hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s) {
       default: return launch_dq<64, 4, 2, false, true>(a, s);
     }
   }
+  if (max(a.d, a.v_d) > 64 && v >= 1700 && v < 1800 && bwd_dkdv_k64_supported(a)) {  // the 64-keys-a-wave dK/dV pass
+    e = launch_dkdv_k64(a, s);
+    if (e != hipSuccess) return e;
+    return launch_dq_pc<128>(a, s);
+  }
   if (max(a.d, a.v_d) > 64 && v >= 0) {
     e = launch_dkdv_pc<128>(a, s);
     if (e != hipSuccess) return e;

@@ -91,6 +91,10 @@ bool fwd_f64_supported(const FwdArgs& a);
 hipError_t launch_fwd_f64(const FwdArgs& a, hipStream_t s);
 bool bwd_f64_supported(const BwdArgs& a);
 hipError_t launch_bwd_f64(const BwdArgs& a, hipStream_t s);
+// dK / dV pass at D = 128 with 64 keys a wave (one wave per SIMD, dK / dV in AGPRs) —
+// diag/fa_bwd_f16_k64.hip (diagnostic library only: FA_BWD_VARIANT 1700)
+bool bwd_dkdv_k64_supported(const BwdArgs& a);
+hipError_t launch_dkdv_k64(const BwdArgs& a, hipStream_t s);
 // two-pass fp16 backward (dK/dV key-outer + dQ query-outer, no atomics) — fa_bwd_f16_fast.hip
 bool bwd_f16_fast_supported(const BwdArgs& a);
 hipError_t launch_bwd_f16_fast(const BwdArgs& a, hipStream_t s);
