@@ -669,6 +669,31 @@ def test_f16_forward_structures_d128(monkeypatch, diag_lib, variant, policy, seq
              bwd=False, seed=int(variant) + d + ws)
 
 
+# the one-wave D = 128 gap-stream forward (csrc/diag/fa_fwd_f16_gap128.hip, FA_FWD_VARIANT=2700): full,
+# causal (the heavy / light pairs), 1d local and 2d interval rules, lengths off the 256-query block and the
+# 64-key tile, d != v_d, channels below 128
+GAP128_CASES = [
+    ("full", 1, "none_front", (264,), (136,), 1, False, 128, 128),
+    ("full", 1, "none_front", (300,), (1000,), 1, False, 96, 128),
+    ("full", 1, "none_front", (1000,), (4096,), 1, False, 128, 128),
+    ("full", 1, "scale_end", (77,), (3000,), 1, False, 120, 100),
+    ("full", 1, "none_front", (64,), (8,), 1, False, 128, 128),
+    ("causal", 1, "none_front", (600,), (600,), 1, False, 128, 128),
+    ("causal", 1, "none_front", (2048,), (2048,), 1, False, 128, 128),
+    ("causal", 1, "scale_end", (328,), (776,), 1, False, 96, 128),
+    ("local", 1, "none_front", (1000,), (1000,), 70, False, 128, 128),
+    ("local", 1, "scale_front", (520,), (264,), 40, True, 128, 80),
+    ("causal", 2, "scale_front", (8, 24), (16, 16), 1, False, 128, 128),
+]
+
+
+@pytest.mark.parametrize("policy,seq_dims,mode,qs,ks,ws,causal,d,vd", GAP128_CASES)
+def test_f16_forward_gap_stream_d128(monkeypatch, diag_lib, policy, seq_dims, mode, qs, ks, ws, causal, d, vd):
+    monkeypatch.setenv("FA_FWD_VARIANT", "2700")
+    run_case(np.float16, policy, seq_dims, mode, (2, 2), d, vd, qs, ks, ws=ws, ls=0, causal=causal, bwd=False,
+             seed=2700 + d + vd + qs[0] + ws)
+
+
 # the 64-keys-a-wave dK/dV pass (csrc/diag/fa_bwd_f16_k64.hip, FA_BWD_VARIANT=1700): full, causal and
 # 1d local windows at d in (64, 128], lengths off the 256-key block and the 32-query tile, nq != nk
 K64_CASES = [

@@ -493,6 +493,7 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
   if (fwd_f16_pp_supported(a) && v >= 2000 && v < 2200) return launch_fwd_f16_pp(a, s);  // 21xx: its ablations
   if (fwd_f16_pingpong_supported(a) && v == 2200) return launch_fwd_f16_pingpong(a, s);
   if (fwd_f16_gap_supported(a) && v >= 2600 && v < 2700) return launch_fwd_f16_gap(a, s);  // 26xx: its ablations
+  if (fwd_f16_gap128_supported(a) && v >= 2700 && v < 2800) return launch_fwd_f16_gap128(a, s);
   if (fwd_f16_pingpong128_supported(a) && v == 2301) return launch_fwd_f16_pingpong128(a, s);
   if (d64 && v == 1814) return launch_fast_t<64, 8, kFPrio | kFLateV | kFTpb2>(a, s);
   if (v == 146) return d64 ? launch_fast_t<64, 4, kFPrio | kFLateV>(a, s) : launch_fast_t<128, 4, kFPrio | kFLateV>(a, s);
@@ -506,8 +507,11 @@ hipError_t launch_fwd_f16_fast(const FwdArgs& a, hipStream_t s) {
   // ping-pong kernel (two wave groups alternating MFMA / softmax phases): the default for
   // d <= 64 under the full policy (c2: 948 vs 904 TF/s for the 8-wave kernel below)
   if (tuned && a.rule.policy == 0 && fwd_f16_pingpong_supported(a)) return launch_fwd_f16_pingpong(a, s);
-  // d in (64, 128]: the ping-pong kernel is the default for the full and causal policies (c3
-  // forward: 2.52 vs 3.16 ms for the 4-wave kernel below); local windows keep the 4-wave blocks
+  // d in (64, 128], full and causal policies: the one-wave gap-stream kernel (c3 forward 2.29 against
+  // 2.40 ms for the ping-pong below, full policy at c3's shape 3.95 against 4.34: DESIGN.md §3.0b), then the
+  // ping-pong (c3 forward: 2.52 vs 3.16 ms for the 4-wave kernel below) where it does not fit; local windows
+  // keep the 4-wave blocks
+  if (tuned && a.rule.policy != 2 && fwd_f16_gap128_supported(a)) return launch_fwd_f16_gap128(a, s);
   if (tuned && a.rule.policy != 2 && fwd_f16_pingpong128_supported(a)) return launch_fwd_f16_pingpong128(a, s);
   if (d64) {
     // tuned on MI355X: full-length key loops 8 waves x 32 queries, two key tiles per barrier;

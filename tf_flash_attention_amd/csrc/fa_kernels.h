@@ -65,6 +65,9 @@ hipError_t launch_fwd_f16_pingpong(const FwdArgs& a, hipStream_t s);
 // diag/fa_fwd_f16_gap.hip (diagnostic library only: FA_FWD_VARIANT 26xx)
 bool fwd_f16_gap_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_gap(const FwdArgs& a, hipStream_t s);
+// one-wave gap-stream fp16 forward for 64 < max(d, v_d) <= 128 (full / causal default) — fa_fwd_f16_gap128.hip
+bool fwd_f16_gap128_supported(const FwdArgs& a);
+hipError_t launch_fwd_f16_gap128(const FwdArgs& a, hipStream_t s);
 // ping-pong fp16 forward for 64 < max(d, v_d) <= 128 — fa_fwd_f16_pingpong128.hip
 bool fwd_f16_pingpong128_supported(const FwdArgs& a);
 hipError_t launch_fwd_f16_pingpong128(const FwdArgs& a, hipStream_t s);

@@ -1,5 +1,5 @@
 """A/B timing of forward structure variants in ONE process (interleaved rounds),
-selected through FA_FWD_VARIANT.  Usage: python tools/fwd_variants.py [config] v1 v2 ..."""
+selected through FA_FWD_VARIANT.  Usage: [FV_POLICY=full|causal] python tools/fwd_variants.py [config] v1 v2 ..."""
 import json
 import os
 import sys
@@ -21,6 +21,7 @@ def main():
     variants = args or ["-1"]
     cfg = bench.CONFIGS[cfgname]
     policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, _ = cfg
+    policy = os.environ.get("FV_POLICY", policy)  # e.g. FV_POLICY=full: config 3's shape without the mask
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(1234)
     b = int(np.prod(batch))
