@@ -329,17 +329,33 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_gap128_kernel(FwdArgs a) 
         }
         return;
       }
-      const int k0 = tk0(it);
-      const int lim = nk - k0 - 8 * h;     // POL 0: offset o is in range iff o < lim
-      const int base = k0 + 8 * h - X.klo;  // POL 1: allowed iff base + o in [0, kspan)
+      // mixed tiles, arithmetically (as fa_fwd_f16_band.hip): key k0 + 8h + off is allowed iff
+      // 0 <= v < kspan, v = k0 + 8h - klo + off (POL 0: klo = 0, kspan = nk, the tail only), so
+      // min(s, (v + 0.5)·2^100) (an edge below) and min(s, (kspan - v - 0.5)·2^100) (an edge above) keep an
+      // allowed score and take a disallowed one to <= -2^99: one fma and one min per score and edge, no
+      // compare (the select form cost a compare, a wait state and a cndmask per score)
+      const int k0 = tk0(it), k1 = k0 + kBN - 1;
+      const int klo = POL != 0 ? X.klo : 0, kspan = POL != 0 ? X.kspan : nk;
+      const bool lo = POL != 0 && X.wlo_max > k0;
+      const bool hi = POL != 0 ? (X.whi_min < k1 || k1 >= nk) : true;
+      constexpr float kBig = 0x1p100f;
+      const float fb = (float)(k0 + 8 * h - klo);
+      if (lo) {
+        const float cc = __builtin_fmaf(fb, kBig, 0.5f * kBig);
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int off = 32 * t + 16 * (i >> 3) + (i & 7);
-          const bool ok = (POL != 0) ? ((unsigned)(base + off) < (unsigned)X.kspan) : (off < lim);
-          X.s[t][i] = ok ? X.s[t][i] : kNegInf;
-        }
+          for (int i = 0; i < 16; ++i)
+            X.s[t][i] = fminf(X.s[t][i], __builtin_fmaf(kBig, (float)(32 * t + 16 * (i >> 3) + (i & 7)), cc));
+      }
+      if (hi) {
+        const float cc = __builtin_fmaf((float)kspan - fb, kBig, -0.5f * kBig);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            X.s[t][i] = fminf(X.s[t][i], __builtin_fmaf(-kBig, (float)(32 * t + 16 * (i >> 3) + (i & 7)), cc));
+      }
     };
     auto exp_cvt = [&](Blk& X) __attribute__((always_inline)) {
 #pragma unroll
@@ -364,7 +380,8 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_gap128_kernel(FwdArgs a) 
       const float pold = (float)__builtin_elementwise_maximum(pmr_old[0], pmr_old[1]);
       X.m_max = fmaxf(X.m_max, fmaxf(X.m_run + mtf, X.m_run + __log2f(pold)));
       const bool unset = X.thr < 0.f;
-      const bool seed = unset && (mtf > X.thr);
+      // (a masked score sits at or below -2^99: a row max below -2^98 means nothing allowed yet)
+      const bool seed = unset && (mtf > -0x1p98f);
       const float delta = unset ? (seed ? mtf : 0.f) : fmaxf(mtf, 0.f);
       const float alpha = unset ? 1.f : __builtin_amdgcn_exp2f(-delta);
       X.m_run += delta;
