@@ -108,8 +108,9 @@ struct Blk {
 #define G2_MAX3 "\n\tv_pk_maximum3_f16 %[pm], %[pm], %[pa], %[pb]"
 #define G2_MAX2 "\n\tv_pk_max_f16 %[pm], %[pa], %[pb]"
 
-// LAY 0: V(i)'s fragment reads one a gap over segment A's gaps 0-15, the DMA pieces in segment B's odd gaps
-// 17-31; LAY 1 (FA_FWD_VARIANT 2701): the reads two a gap in gaps 0-7, the DMA pieces in segment A's gaps 8-15
+// LAY 0: V(i)'s fragment reads one a gap over segment A's gaps 0-15, the DMA pieces in the four lightest gaps of
+// each segment (28-31: folds, max, predicate), K's in segment A, V's in segment B; LAY 1 (FA_FWD_VARIANT 2701):
+// the reads two a gap in gaps 0-7, the DMA pieces in segment A's gaps 8-15
 template <int POL, int LAY = 0>
 __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_gap128_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_gap128_kernel(FwdArgs a) 
     //   30          : the tile's max over the two halves, the epoch max of P
     //   31          : the rebase predicate (an SGPR pair): the check after the segment is one scalar branch
     float ft0 = 0.f;  // the even gap's exponential, converted in the odd gap
-    int cur_it = 0;   // (LAY 1: the step, for segment A's DMA pieces)
+    int cur_it = 0;   // (the step, for segment A's DMA pieces)
     auto gap = [&](Blk& X, Blk& Y, auto G_) __attribute__((always_inline)) {
       constexpr int g = decltype(G_)::value;
       constexpr bool full = g >= 24 && g < 28;
@@ -518,7 +519,8 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_gap128_kernel(FwdArgs a) 
     };
 
     // segment A of step it (slot c = it mod 4): MFMAs of A, softmax of B(it); V(it)'s fragments one a gap
-    // over gaps 0-15, quarters 0-1 first (their PV MFMAs run in gaps 16-23, quarters 2-3 in 24-31)
+    // over gaps 0-15, quarters 0-1 first (their PV MFMAs run in gaps 16-23, quarters 2-3 in 24-31); the DMA
+    // pieces of K(it+4) in gaps 28-31 (LAY 0)
     auto seg_a = [&](auto C_) __attribute__((always_inline)) {
       constexpr int c = decltype(C_)::value;
       auto body = [&](auto G_) __attribute__((always_inline)) {
@@ -528,6 +530,7 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_gap128_kernel(FwdArgs a) 
           if constexpr (g == 24) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): quarters 2-3
           gap(A, B, G_);
           if constexpr (g < 16) read_vf(IC<c>{}, IC<(4 * ((g & 7) >> 1) + 2 * (g >> 3) + (g & 1))>{});
+          if constexpr (g >= 28) dma_k(g - 28, tk0(cur_it + 4), c);
         } else {
           if constexpr (g == 16) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): V(it)
           gap(A, B, G_);
@@ -545,7 +548,7 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_gap128_kernel(FwdArgs a) 
       seg_end(A);
     };
     // segment B of step it: MFMAs of B, softmax of A(it+1); K(it+2)'s fragments in gaps 2-17, the DMA
-    // pieces of K(it+4) / V(it+2) in the odd gaps 17-31
+    // pieces of V(it+2) in gaps 28-31 (LAY 0)
     auto seg_b = [&](auto C_, int it) __attribute__((always_inline)) {
       constexpr int c = decltype(C_)::value;
       const int kk = tk0(it + 4), kv = tk0(it + 2);
@@ -554,8 +557,7 @@ __global__ __launch_bounds__(kNW * 64, 1) void fwd_f16_gap128_kernel(FwdArgs a) 
         constexpr int g = decltype(G_)::value;
         gap(B, A, G_);
         if constexpr (g >= 2 && g < 18) read_kf((c + 2) % kNS, IC<((g - 2) >> 1)>{}, IC<((g - 2) & 1)>{});
-        if constexpr (LAY == 0 && g >= 17 && (g & 1) && g < 25) dma_k((g - 17) >> 1, kk, c);
-        if constexpr (LAY == 0 && g >= 25 && (g & 1)) dma_v((g - 25) >> 1, kv, (c + 2) % kNS);
+        if constexpr (LAY == 0 && g >= 28) dma_v(g - 28, kv, (c + 2) % kNS);
         __builtin_amdgcn_sched_barrier(0);
       };
       A.pmr_old = A.pmr;
