@@ -12,23 +12,22 @@
 //   segment A of step i : Sᵀ A(i+1) (16 MFMAs), PV A(i) (16)  |  softmax B(i), row sums of P_B(i-1)
 //   segment B of step i : Sᵀ B(i+1) (16 MFMAs), PV B(i) (16)  |  softmax A(i+1), row sums of P_A(i)
 //
-// Gap g of a segment: MFMA g, then half of the other block's P dword g/2: even gaps its first v_exp_f32
-// and the first v_fma_mix_f32 row-sum step of the dword's previous value (plus a packed-max fold every
-// fourth gap), odd gaps the second exponential, the second row-sum step and the v_cvt_pk_f16_f32 that
-// overwrites the dword (one instruction between the exponential and its use: the transcendental's
-// forwarding wait state).
+// Gap g of a segment: MFMA g and its share of the other block's softmax (the table at `gap` below): in gaps
+// 0-23 half of P dword g/2 a gap (one v_exp_f32, preceded by the v_sub of the running reference: the scores
+// leave the MFMA relative to 0), in gaps 24-27 one whole dword each, then the last packed-max folds, the
+// tile's max and the rebase predicate (an SGPR pair), so the check after a segment is one scalar branch.
 //
-// Registers (one wave per SIMD, 512): VGPRs hold both blocks' scores, -m broadcasts and P, and the whole
-// K(i+1) tile's fragments (read once, used by both segments); AGPRs hold both blocks' O (128), Q (64) and
-// the whole V(i) tile's fragments (64).  No register is left for staging, so K / V reach LDS by LDS-DMA
-// (inline-asm buffer_load ... lds, two steps ahead, four-slot rings, counted vmcnt waits; the lanes'
-// source chunks permuted so each wave's contiguous 1 KB is the swizzled image).  LDS: K ring 64 KB, V ring
-// 64 KB; the Q image [128][256] of the prologue lies over the K ring.
+// Registers (one wave per SIMD, 512): VGPRs hold both blocks' scores and P, and the whole K(i+1) tile's
+// fragments (read once, used by both segments); AGPRs hold both blocks' O (128), Q (64) and the whole V(i)
+// tile's fragments (64).  No register is left for staging, so K / V reach LDS by LDS-DMA (inline-asm
+// buffer_load ... lds, two steps ahead, four-slot rings, counted vmcnt waits; the lanes' source chunks
+// permuted so each wave's contiguous 1 KB is the swizzled image).  LDS: K ring 64 KB, V ring 64 KB; the Q
+// image [128][256] of the prologue lies over the K ring.
 //
-// Memory operations per step: V(i)'s 16 fragment reads in segment A's gaps 0-7 (asm ds_read_b128 into
-// AGPRs, waited by an lgkmcnt(0) before the PV MFMAs), the eight DMA pieces of K(i+4) / V(i+2) in gaps
-// 8-15, K(i+2)'s 32 transposed reads in segment B's gaps 2-17 (each into the registers the Sᵀ MFMA two
-// gaps back finished with).  One barrier a step.
+// Memory operations per step: V(i)'s 16 fragment reads one a gap in segment A's gaps 0-15 (asm ds_read_b128
+// into AGPRs, waited by lgkmcnt before the PV MFMAs that use them), K(i+2)'s 32 transposed reads in segment
+// B's gaps 2-17 (each into the registers the Sᵀ MFMA two gaps back finished with), the eight DMA pieces of
+// K(i+4) / V(i+2) in the four lightest gaps of each segment (28-31).  One barrier a step.
 //
 // Rules: the full policy and interval rules (causal, 1d local), with the heavy / light block pairing of
 // fa_fwd_f16_pingpong128.hip.  Numerics as fa_fwd_f16_gap.hip.  Replaces the reference's ForwardImpl
