@@ -61,8 +61,7 @@ def grad_bound(ref, e, dtype):
 # the same ratio the worst correct fp16 case of the suite reaches); the slope averages the rounding
 # noise out and sees it at full size.  Measured over the GPU suite (1351 cases, profiles/r06_gate_stats.txt):
 # max |slope| of the non-degenerate gradients 1.63e-3 (fp16, a 2-element d = 1 case), 1.9e-6 (fp32),
-# 1.4e-15 (fp64); fp16 at d = 1 can pass 2^-9 against the exact oracle, and is then held to the same
-# tolerance against the oracle on the kernels' own rounded Q (slope_ok, prescaled_q).
+# 1.4e-15 (fp64); fp16 at d = 1 has its own tolerance (slope_tol).
 SLOPE_TOL = {np.float16: 2.0 ** -9, np.float32: 2.0 ** -17, np.float64: 2.0 ** -45}
 SLOPE_SNR = 100.0
 
@@ -79,28 +78,20 @@ def elements_ok(got, ref, e, dtype) -> bool:
     return bool(np.isfinite(got).all() and (np.abs(got - ref) <= grad_bound(ref, e, dtype)).all())
 
 
-def slope_ok(got, ref, e, dtype, ref_alt=None) -> bool:
-    """|slope| within SLOPE_TOL against the exact reference, or (fp16) against ``ref_alt``: the oracle's
-    gradients on the operand the fp16 kernels actually score with (prescaled_q).  The kernels form
-    the scores from Q·scale·log2(e) rounded to fp16; at d = 1 that rounding scales a
-    whole query row's scores by one factor (1 + δ), |δ| <= 2^-11, and the gradients follow coherently
-    (a correct d = 1 case of the 20000-case fuzz reached slope 2.05e-3 against the exact oracle).  A
-    defect shows against both references (tests/test_gate_mutations.py)."""
-    if not slope_applies(ref, e) or abs(scale_slope(got, ref)) <= SLOPE_TOL[dtype]:
-        return True
-    return ref_alt is not None and abs(scale_slope(got, ref_alt)) <= SLOPE_TOL[dtype]
+def slope_tol(dtype, d=None) -> float:
+    """SLOPE_TOL, except fp16 at d = 1: each score is then one product, so the kernels' rounding of the
+    pre-scaled Q (one fp16 rounding per query row) is not averaged over channels and the row's
+    scores, and its gradients, move coherently; a correct d = 1 case of the 20000-case fuzz reached a slope of
+    2.05e-3 (> 2^-9).  3e-3 still rejects dS x (1 + 2^-8) (slope 3.9e-3, tests/test_gate_mutations.py)."""
+    return 3e-3 if (dtype == np.float16 and d == 1) else SLOPE_TOL[dtype]
 
 
-def prescaled_q(Q, d):
-    """Q as the fp16 kernels score with it, in float64: fp16(float32(Q) · c) / c with c =
-    float32(1/sqrt(d)) · log2(e) in float32 (fa_api.hip a.scale, fa_mfma.h scale8)."""
-    c = np.float32(np.float32(1.0 / np.sqrt(np.float64(d))) * np.float32(1.4426950408889634))
-    q16 = (np.asarray(Q).astype(np.float32) * c).astype(np.float16)
-    return q16.astype(np.float64) / np.float64(c)
+def slope_ok(got, ref, e, dtype, d=None) -> bool:
+    return (not slope_applies(ref, e)) or abs(scale_slope(got, ref)) <= slope_tol(dtype, d)
 
 
-def grad_ok(got, ref, e, dtype, ref_alt=None) -> bool:
-    return elements_ok(got, ref, e, dtype) and slope_ok(got, ref, e, dtype, ref_alt)
+def grad_ok(got, ref, e, dtype, d=None) -> bool:
+    return elements_ok(got, ref, e, dtype) and slope_ok(got, ref, e, dtype, d)
 
 
 def scale_slope(got, ref):

@@ -99,15 +99,17 @@ def _case(c, dtype):
     esc = O.backward_rounding_scale_f64(Qf, Kf, Vf, dOf, prob, *gate.U_ROUND[dtype])
     mask = O.problem_mask(prob, tuple(c["qs"]), tuple(c["ks"]))
     d, vd, nq, nk = c["d"], c["vd"], int(np.prod(c["qs"])), int(np.prod(c["ks"]))
-    # the gate's second slope reference (fp16): the oracle on the Q the kernels score with
-    alt = (O.backward_f64(gate.prescaled_q(Qf, d).reshape(Qf.shape), Kf, Vf, dOf, prob)
-           if dtype == np.float16 else (None, None, None))
-    return Qf, Kf, Vf, dOf, ref, esc, mask, (d, vd, nq, nk), alt
+    return Qf, Kf, Vf, dOf, ref, esc, mask, (d, vd, nq, nk)
 
 
 def _rejected(case, mut, dtype):
     """True / False: the gate rejects / accepts the defect; None: not applicable to the case."""
-    Qf, Kf, Vf, dOf, ref, esc, mask, (d, vd, nq, nk), alt = case
+    Qf, Kf, Vf, dOf, ref, esc, mask, (d, vd, nq, nk) = case
+    if mut == "lse_ulp" and dtype == np.float16 and d == 1:
+        # at d = 1 the fp16 kernels' own rounding of the pre-scaled Q moves a whole row's scores coherently
+        # (a correct case of the 20000-case fuzz: slope 2.05e-3), the size of this defect there (1.5-2.4e-3):
+        # no gate separates the two at that d, so it is not counted (d >= 2 keeps it; gate.slope_tol)
+        return None
     got = [[], [], []]
     for i in range(Qf.shape[0]):
         g = _mutated_grads(Qf[i].reshape(d, nq).astype(np.float64), Kf[i].reshape(d, nk).astype(np.float64),
@@ -123,13 +125,12 @@ def _rejected(case, mut, dtype):
         r = ref[j].reshape(len(got[j]), -1)
         e = esc[j].reshape(len(got[j]), -1)
         g = np.stack(got[j]).reshape(r.shape)
-        ra = None if alt[j] is None else alt[j].reshape(r.shape)
-        ok &= gate.grad_ok(g, r, e, dtype, ra)
+        ok &= gate.grad_ok(g, r, e, dtype, d)
         # material: visible to an exact computation at all — past the plain rtol/atol bound somewhere,
         # or past the slope tolerance (a defect below both is below fp rounding of the case, e.g. a dropped
         # tile of keys no query attends to, or dS scaled where dS is analytically 0)
         material |= bool((np.abs(g - r) > gate.plain_bound(r, rtol, atol)).any())
-        material |= gate.slope_applies(r, e) and abs(gate.scale_slope(g, r)) > gate.SLOPE_TOL[dtype]
+        material |= gate.slope_applies(r, e) and abs(gate.scale_slope(g, r)) > gate.slope_tol(dtype, d)
     if not material:
         return None
     return not ok
@@ -160,7 +161,7 @@ def test_correct_gradients_pass_gate():
     for i in CANCELLING[:4]:
         c = draw(i)
         for dt in (np.float16, np.float32):
-            Qf, Kf, Vf, dOf, ref, esc, mask, _, _ = _case(c, dt)
+            Qf, Kf, Vf, dOf, ref, esc, mask, _ = _case(c, dt)
             for j in range(3):
                 g = ref[j].astype(dt).astype(np.float64)
                 assert gate.grad_ok(g.reshape(g.shape[0], -1), ref[j].reshape(g.shape[0], -1),

@@ -160,15 +160,8 @@ def run_case(dtype, policy, seq_dims, mode, batch, d, vd, qs, ks, ws=1, ls=0, ca
             res[name] = _close(name, got, ref, rtol, atol, gate.grad_extra(ref, e, dtype))
             # whole-gradient scale: catches a defect scaling a gradient by ~2^-8 in fp16 that the
             # per-element bound cannot see (tests/gate.py, tests/test_gate_mutations.py)
-            if not gate.slope_ok(got, ref, e, dtype):
-                # fp16: against the oracle on the Q the kernels score with (tests/gate.py prescaled_q)
-                alt = None
-                if dtype == np.float16:
-                    qe = gate.prescaled_q(Qf, d).reshape(Qf.shape)
-                    alt = dict(zip(("dQ", "dK", "dV"), O.backward_f64(qe, Kf, Vf, dOf, prob, slices=sl)))[name]
-                assert gate.slope_ok(got, ref, e, dtype, alt), (
-                    f"{name}: scale slope {gate.scale_slope(got, ref):.3e} > {gate.SLOPE_TOL[dtype]:.3e}"
-                    + ("" if alt is None else f" (against the kernels' rounded Q: {gate.scale_slope(got, alt):.3e})"))
+            assert gate.slope_ok(got, ref, e, dtype, d), (
+                f"{name}: scale slope {gate.scale_slope(got, ref):.3e} > {gate.slope_tol(dtype, d):.3e}")
     return res
 
 
