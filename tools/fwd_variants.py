@@ -1,5 +1,5 @@
 """A/B timing of forward structure variants in ONE process (interleaved rounds),
-selected through FA_FWD_VARIANT.  Usage: [FV_POLICY=full|causal] python tools/fwd_variants.py [config] v1 v2 ..."""
+selected through FA_FWD_VARIANT.  Usage: [FV_POLICY=full|causal] [FV_D=d] [FV_BATCH=b,h] python tools/fwd_variants.py [config] v1 v2 ..."""
 import json
 import os
 import sys
@@ -22,6 +22,9 @@ def main():
     cfg = bench.CONFIGS[cfgname]
     policy, seq_dims, dt, batch, d, qs, ks, sync, ws, ls, causal, bwd, _ = cfg
     policy = os.environ.get("FV_POLICY", policy)  # e.g. FV_POLICY=full: config 3's shape without the mask
+    d = int(os.environ.get("FV_D", d))  # e.g. FV_D=128: config 4's band at d = 128
+    if "FV_BATCH" in os.environ:  # e.g. FV_BATCH=8,16
+        batch = tuple(int(x) for x in os.environ["FV_BATCH"].split(","))
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(1234)
     b = int(np.prod(batch))
