@@ -62,7 +62,10 @@ def grad_bound(ref, e, dtype):
 # noise out and sees it at full size.  Measured over the GPU suite (1351 cases, profiles/r06_gate_stats.txt):
 # max |slope| of the non-degenerate gradients 1.63e-3 (fp16, a 2-element d = 1 case), 1.9e-6 (fp32),
 # 1.4e-15 (fp64); fp16 at d = 1 has its own tolerance (slope_tol).
-SLOPE_TOL = {np.float16: 2.0 ** -9, np.float32: 2.0 ** -17, np.float64: 2.0 ** -45}
+# fp32 2^-15: a correct d = 256 case of five queries and five keys in a window (fuzz seed 28600) reached 7.7e-6
+# in dK (> 2^-17), two cancelling large elements over rounding-level ones; every injected fp32 defect is
+# still >= 1e-3 (tests/test_gate_mutations.py)
+SLOPE_TOL = {np.float16: 2.0 ** -9, np.float32: 2.0 ** -15, np.float64: 2.0 ** -45}
 SLOPE_SNR = 100.0
 
 
