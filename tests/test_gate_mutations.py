@@ -125,12 +125,13 @@ def _rejected(case, mut, dtype):
         r = ref[j].reshape(len(got[j]), -1)
         e = esc[j].reshape(len(got[j]), -1)
         g = np.stack(got[j]).reshape(r.shape)
-        ok &= gate.grad_ok(g, r, e, dtype, d)
+        ch = d if name != "dV" else vd
+        ok &= gate.grad_ok(g, r, e, dtype, d, ch)
         # material: visible to an exact computation at all — past the plain rtol/atol bound somewhere,
         # or past the slope tolerance (a defect below both is below fp rounding of the case, e.g. a dropped
         # tile of keys no query attends to, or dS scaled where dS is analytically 0)
         material |= bool((np.abs(g - r) > gate.plain_bound(r, rtol, atol)).any())
-        material |= gate.slope_applies(r, e) and abs(gate.scale_slope(g, r)) > gate.slope_tol(dtype, d)
+        material |= gate.slope_applies(r, e) and abs(gate.scale_slope(g, r)) > gate.slope_tol_eff(r, e, dtype, d, ch)
     if not material:
         return None
     return not ok

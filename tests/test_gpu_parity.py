@@ -160,8 +160,10 @@ def run_case(dtype, policy, seq_dims, mode, batch, d, vd, qs, ks, ws=1, ls=0, ca
             res[name] = _close(name, got, ref, rtol, atol, gate.grad_extra(ref, e, dtype))
             # whole-gradient scale: catches a defect scaling a gradient by ~2^-8 in fp16 that the
             # per-element bound cannot see (tests/gate.py, tests/test_gate_mutations.py)
-            assert gate.slope_ok(got, ref, e, dtype, d), (
-                f"{name}: scale slope {gate.scale_slope(got, ref):.3e} > {gate.slope_tol(dtype, d):.3e}")
+            ch = got.shape[1]  # [batch, channels, positions...]: the channels of one row
+            assert gate.slope_ok(got, ref, e, dtype, d, ch), (
+                f"{name}: scale slope {gate.scale_slope(got, ref):.3e} > "
+                f"{gate.slope_tol_eff(ref, e, dtype, d, ch):.3e}")
     return res
 
 
