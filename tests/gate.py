@@ -106,8 +106,24 @@ def row_coherent_slope(ref, e, ch) -> float:
     return float(np.sqrt(np.sum(per_row * per_row)) / rr)
 
 
+def coherent_slope(ref, e) -> float:
+    """The slope of a rounding error of size e coherent over the whole gradient: <e, |ref|> / <ref, ref>."""
+    ref = np.asarray(ref, dtype=np.float64)
+    rr = float(np.sum(ref * ref))
+    return float(np.sum(np.abs(ref) * np.asarray(e, dtype=np.float64)) / rr) if rr > 0.0 else 0.0
+
+
 def slope_tol_eff(ref, e, dtype, d=None, ch=None) -> float:
-    return max(slope_tol(dtype, d), row_coherent_slope(ref, e, ch))
+    """The slope tolerance of one gradient.  fp16 at d = 1: each score is one product of a query and a key,
+    so the rounding of the pre-scaled query moves every score of its row by the same relative amount, and
+    that row's error reaches every key's dK / dV as well as its own dQ: the rounding is coherent over the
+    whole gradient, not per row (a correct full-window causal case, seed 72261: 577 queries, 418 keys, dK
+    slope -3.43e-3 against this bound's 8.36e-3).  Everywhere else: slope_tol, or the row-coherent bound
+    where a gradient rests on few rows."""
+    tol = max(slope_tol(dtype, d), row_coherent_slope(ref, e, ch))
+    if dtype == np.float16 and d == 1:
+        tol = max(tol, coherent_slope(ref, e))
+    return tol
 
 
 def slope_ok(got, ref, e, dtype, d=None, ch=None) -> bool:
