@@ -169,3 +169,34 @@ def test_correct_gradients_pass_gate():
                 g = ref[j].astype(dt).astype(np.float64)
                 assert gate.grad_ok(g.reshape(g.shape[0], -1), ref[j].reshape(g.shape[0], -1),
                                     esc[j].reshape(g.shape[0], -1), dt)
+
+
+def test_slope_bounds():
+    """The two coherent-rounding slope bounds of tests/gate.py: with one row carrying the gradient the
+    row-coherent bound is the whole-gradient one; over n equal rows it falls as 1/sqrt(n); fp16 at d = 1
+    takes the whole-gradient bound, every other (dtype, d) only the row-coherent one."""
+    rng = np.random.default_rng(0)
+    ch = 64
+    one = np.zeros((1, ch, 8))
+    one[0, :, 3] = rng.uniform(-1, 1, ch)
+    e = np.full_like(one, 1e-4)
+    assert math.isclose(gate.row_coherent_slope(one, e, ch), gate.coherent_slope(one, e), rel_tol=1e-12)
+    rows = np.repeat(one[:, :, 3:4], 16, axis=2)
+    er = np.full_like(rows, 1e-4)
+    assert math.isclose(gate.row_coherent_slope(rows, er, ch), gate.coherent_slope(rows, er) / 4.0, rel_tol=1e-12)
+    # a coherent error of size e in one row passes, the same relative scale error of a 16-row gradient does not
+    e1r = np.zeros_like(one)
+    e1r[0, :, 3] = 2e-3
+    r1 = gate.row_coherent_slope(one, e1r, ch)
+    assert gate.slope_applies(one, e1r) and r1 > gate.SLOPE_TOL[np.float16]
+    assert gate.slope_ok(one * (1.0 + 0.9 * r1), one, e1r, np.float16, d=ch, ch=ch)
+    assert not gate.slope_ok(one * (1.0 + 1.1 * r1), one, e1r, np.float16, d=ch, ch=ch)
+    big = np.repeat(one[:, :, 3:4], 4096, axis=2) * rng.uniform(0.5, 1.5, (1, 1, 4096))
+    eb = np.abs(big) * 2.0 ** -11
+    assert gate.slope_tol_eff(big, eb, np.float16, 64, ch) == gate.SLOPE_TOL[np.float16]
+    assert not gate.slope_ok(big * (1.0 + 2.0 ** -8), big, eb, np.float16, 64, ch)
+    # fp16 d = 1: the whole-gradient bound; fp32 d = 1: not
+    d1 = rng.uniform(-1, 1, (1, 1, 300))
+    e1 = np.abs(d1) * 4e-3
+    assert math.isclose(gate.slope_tol_eff(d1, e1, np.float16, 1, 1), 4e-3, rel_tol=1e-9)
+    assert gate.slope_tol_eff(d1, e1, np.float32, 1, 1) < 4e-3
