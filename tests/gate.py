@@ -158,3 +158,18 @@ def grad_stats(got, ref, e, dtype) -> dict:
                 max_err_over_full=float((err / full).max()) if err.size else 0.0,
                 frac_over_plain=float((err > plain).mean()) if err.size else 0.0,
                 slope=scale_slope(got, ref), ref_rms=float(np.sqrt(np.mean(ref * ref))) if err.size else 0.0)
+
+
+def max_abs_dot(Q, K, mask, chunk=512):
+    """Per slice and query row, max over the row's allowed keys of sum_c |q_c| |k_c| (Q [b, d, nq], K [b, d, nk],
+    mask [nq, nk]; 0 for a row with no allowed key): the scale of the rounding a score, and so the row max,
+    can carry when Q is rounded before the product (tests/test_gpu_parity.py's fp16 m bound)."""
+    b, _, nq = Q.shape
+    out = np.zeros((b, nq))
+    for i in range(b):
+        aq = np.abs(Q[i].astype(np.float64)).T
+        ak = np.abs(K[i].astype(np.float64))
+        for r0 in range(0, nq, chunk):
+            p = aq[r0:r0 + chunk] @ ak
+            out[i, r0:r0 + chunk] = np.where(mask[r0:r0 + chunk], p, 0.0).max(axis=1)
+    return out
